@@ -1,0 +1,263 @@
+/*
+ * pm.h — C-ABI of the MI355X-native photon-mapping hot path (libpm_hip.so).
+ *
+ * This is the drop-in boundary for the three reference boundaries named in
+ * SURVEY.md §8(b):
+ *   B1  process / CLI contract  -> the `photon-mapping`, `photonMapping`,
+ *       `rayTracer` binaries built on top of this library (tools/).
+ *   B2  OWL/OptiX device-program ABI (photon-mapping/include/deviceCode.h:8-43,
+ *       ray-tracer/include/deviceCode.h:10-64, common/src/mesh.h:15-20)
+ *       -> pm_scene_*, pm_trace_photons, pm_render.
+ *   B3  cudaKDTree template API (ray-tracer/src/hostCode.cu:94-95,
+ *       ray-tracer/cuda/shading.h:11-18) -> pm_kdtree_build, pm_knn.
+ *
+ * Conventions (all entry points):
+ *   - extern "C", plain pointers and sizes; no torch / HIP types.
+ *   - every call returns an int status (PM_OK == 0); no aborts.
+ *   - pointers prefixed d_ are DEVICE pointers (caller-owned, e.g. torch
+ *     tensors or hipMalloc); h_ / plain pointers are host memory.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *     Calls that return a host-visible scalar (counts) synchronise the stream.
+ *   - handles (pm_scene, pm_photon_map) own their device memory.
+ *   - single-threaded per handle.
+ * There is NO CPU fallback: every compute entry point runs HIP kernels for
+ * gfx950 and fails with PM_ERR_NO_DEVICE when no GPU is present.
+ */
+#ifndef PM_H_
+#define PM_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PM_ABI_VERSION 1
+
+enum pm_status {
+  PM_OK = 0,
+  PM_ERR_INVALID = 1,     /* bad argument / shape                          */
+  PM_ERR_HIP = 2,         /* HIP runtime error                             */
+  PM_ERR_OOM = 3,         /* device allocation failed                      */
+  PM_ERR_NO_DEVICE = 4,   /* no gfx950 device visible                      */
+  PM_ERR_IO = 5,          /* file could not be opened / parsed             */
+  PM_ERR_CAPACITY = 6,    /* output buffer too small (count still written) */
+  PM_ERR_OVERFLOW = 7     /* traversal stack overflow inside a kernel      */
+};
+
+typedef struct { float x, y, z; } pm_float3;
+typedef struct { int32_t x, y, z; } pm_int3;
+
+/* common/src/mesh.h:6-12  (28 B) */
+typedef struct {
+  pm_float3 albedo;
+  float diffuse, specular, transmission, refraction_idx;
+} pm_material;
+
+/* common/src/mesh.h:22-27 (Mesh) + mesh.h:15-20 (TrianglesGeomData). */
+typedef struct {
+  const pm_float3* vertices;   /* host */
+  int32_t num_vertices;
+  const pm_int3* indices;      /* host, per-mesh vertex indices */
+  int32_t num_triangles;
+  pm_material material;
+} pm_mesh;
+
+/* common/src/world.h:11-27 (LightSource, 64 B). Only POINT_LIGHT is traced,
+ * as in the reference (assetImporter.cxx:122). */
+enum { PM_POINT_LIGHT = 0, PM_SQUARE_LIGHT = 1 };
+typedef struct {
+  int32_t source_type;
+  pm_float3 pos;
+  double power;
+  pm_float3 rgb;
+  pm_float3 normal;
+  double side_length;
+  int32_t num_photons;
+} pm_light;
+
+/* photon-mapping/include/photon.h:5-11 (40 B) — stage-1 output record. */
+typedef struct {
+  pm_float3 pos;
+  pm_float3 dir;
+  int32_t power;               /* never written by the reference */
+  pm_float3 color;
+} pm_photon;
+
+/* ray-tracer/include/photon.h:11-21 (44 B) — cudaKDTree data record. */
+typedef struct {
+  pm_float3 pos;
+  pm_float3 dir;
+  pm_float3 color;
+  float power;
+  uint8_t quantized_normal[3];
+  uint8_t split_dim;
+} pm_kd_photon;
+
+/* cukd::box_t<float3> */
+typedef struct { pm_float3 lower, upper; } pm_box;
+
+/* common/src/camera.h:5-10 */
+typedef struct { pm_float3 pos, dir_00, dir_du, dir_dv; } pm_camera;
+
+/* A ray for the traversal entry points (owl::Ray: origin, direction, tmin, tmax). */
+typedef struct { pm_float3 origin; float tmin; pm_float3 direction; float tmax; } pm_ray;
+/* Closest-hit record: t, mesh (OWL geom index) and primitive (optixGetPrimitiveIndex). */
+typedef struct { float t; int32_t mesh; int32_t prim; int32_t tri; } pm_hit;
+
+/* ---- library / device ---------------------------------------------------- */
+int pm_abi_version(void);
+const char* pm_status_string(int status);
+/* Number of visible HIP devices (0 on a host without a GPU; never fails). */
+int pm_device_count(int32_t* count);
+/* Microseconds of the last kernel(s) of a phase, measured with hipEvents on
+ * the stream the kernels ran on. phase: 0 trace, 1 compaction, 2 kd-build,
+ * 3 render-paths, 4 knn-gather, 5 resolve, 6 bvh-build. */
+int pm_last_phase_us(int32_t phase, double* us);
+
+/* ---- scene (world.cpp:3-58 loadGeometry; OptiX GAS+IAS -> HIP LBVH) ------- */
+typedef struct pm_scene pm_scene;
+typedef struct {
+  int64_t num_triangles;
+  int64_t num_nodes;
+  int32_t num_meshes;
+  int32_t max_depth;          /* deepest BVH leaf */
+  pm_box bounds;
+} pm_scene_stats;
+
+int pm_scene_create(const pm_mesh* meshes, int32_t num_meshes, pm_scene** out);
+int pm_scene_stats_get(const pm_scene* scene, pm_scene_stats* out);
+int pm_scene_destroy(pm_scene* scene);
+/* Closest hit (optixTrace without any-hit) for n rays; miss -> t=+inf, ids -1. */
+int pm_scene_intersect(pm_scene* scene, const pm_ray* d_rays, int64_t n,
+                       pm_hit* d_hits, void* stream);
+/* Shadow rays (TERMINATE_ON_FIRST_HIT): d_occluded[i] = 1 if any hit in (tmin,tmax). */
+int pm_scene_occluded(pm_scene* scene, const pm_ray* d_rays, int64_t n,
+                      int32_t* d_occluded, void* stream);
+
+/* ---- stage 1: photon emission + bounce ----------------------------------
+ * photon-mapping/src/hostCode.cu:72-138 (runPointLightRayGen, runNormal,
+ * runCaustics), photon-mapping/cuda/deviceCode.cu:10-136.
+ * Output order is deterministic: (light, photon id, bounce); the reference's
+ * atomicAdd order (deviceCode.cu:11) is nondeterministic, so parity is on this
+ * canonical order (a permutation of the reference's multiset). */
+typedef struct {
+  int64_t casted_photons;      /* photon-mapper.casted_{diffuse,caustics}_photons */
+  int32_t max_depth;           /* photon-mapper.max_depth */
+  int32_t caustics_mode;       /* 0 = runNormal, 1 = runCaustics */
+  int32_t shard_rank;          /* photon-index sharding across GPUs (0..count-1) */
+  int32_t shard_count;         /* 1 = whole job */
+} pm_trace_params;
+
+/* Photons launched per light: n_L = int(P_L * int(casted / sum P)) (hostCode.cu:86,102-110). */
+int pm_photons_per_light(const pm_light* lights, int32_t num_lights,
+                         int64_t casted_photons, int64_t* h_counts /* num_lights */);
+/* Worst-case number of stored photons for this shard (capacity to allocate). */
+int pm_trace_capacity(const pm_light* lights, int32_t num_lights,
+                      const pm_trace_params* params, int64_t* capacity);
+/* Trace and compact. d_out receives *count photons (device). If capacity is
+ * too small PM_ERR_CAPACITY is returned with *count set to the needed size. */
+int pm_trace_photons(pm_scene* scene, const pm_light* lights, int32_t num_lights,
+                     const pm_trace_params* params, pm_photon* d_out,
+                     int64_t capacity, int64_t* count, void* stream);
+
+/* ---- stage 2a: kd-tree (cukd::buildTree, hostCode.cu:94-95) -------------- */
+/* In place: reorders d_photons into a left-balanced implicit kd-tree (children
+ * 2i+1, 2i+2) with split_dim set per node (has_explicit_dim, photon.h:23-40);
+ * writes the point bounds to *d_bounds (device) if non-NULL. */
+int pm_kdtree_build(pm_kd_photon* d_photons, int64_t n, pm_box* d_bounds, void* stream);
+
+/* Photon map = kd-tree + gather payload, built from stage-1 photon arrays the
+ * way loadPhotons does (hostCode.cu:54-99): map = a[0..na) (power_a) ++
+ * b[0..nb) (power_b). Original index = position in that concatenation. */
+typedef struct pm_photon_map pm_photon_map;
+int pm_photon_map_create(const pm_photon* d_a, int64_t na, float power_a,
+                         const pm_photon* d_b, int64_t nb, float power_b,
+                         pm_photon_map** out, void* stream);
+int pm_photon_map_size(const pm_photon_map* map, int64_t* n);
+/* Copy the map out in kd order as reference kd records (power, split_dim set). */
+int pm_photon_map_export(const pm_photon_map* map, pm_kd_photon* d_out, void* stream);
+int pm_photon_map_destroy(pm_photon_map* map);
+
+/* ---- stage 2b: kNN + radiance estimate ----------------------------------
+ * cukd::stackBased::knn<HeapCandidateList<k>> (shading.h:11-18): exact k
+ * nearest photons with d^2 < max_radius^2, ordered by (d^2, original index);
+ * empty slots id -1. d_maxd2[q] = k-th d^2, or max_radius^2 if fewer found.
+ * d_ids / d_d2 are [nq][k] (d_d2 may be NULL). k <= 256. */
+int pm_knn(const pm_photon_map* map, const pm_float3* d_queries, int64_t nq,
+           int32_t k, float max_radius, int32_t* d_ids, float* d_d2,
+           float* d_maxd2, void* stream);
+/* gatherPhotons (shading.h:93-121), k = 50, radius 100, cone filter 1.1. */
+int pm_gather(const pm_photon_map* map, const pm_float3* d_points,
+              const float* d_brdf, int64_t nq, pm_float3* d_out, void* stream);
+
+/* ---- stage 2c: render (simpleRayGen, ray-tracer/cuda/deviceCode.cu:25-231) */
+typedef struct {
+  int32_t width, height;       /* ray-tracer.fb_size */
+  int32_t samples_per_pixel;   /* ray-tracer.samples_per_pixel */
+  int32_t max_depth;           /* ray-tracer.depth */
+  pm_camera camera;
+  pm_float3 sky_colour;        /* ray-tracer.sky_colour */
+  int32_t tile_rank;           /* image-tile sharding (16x16 tiles round robin) */
+  int32_t tile_count;          /* 1 = whole image */
+} pm_render_params;
+
+/* setupCamera (ray-tracer/src/hostCode.cu:100-108), cos(fovy) scaling kept. */
+int pm_camera_setup(pm_float3 look_from, pm_float3 look_at, pm_float3 look_up,
+                    float fovy, int32_t width, int32_t height, pm_camera* out);
+/* Renders into d_rgba (uint32 [H][W], row H-y layout of deviceCode.cu:224-230;
+ * rows/tiles not rendered are left untouched) and, if non-NULL, d_rgb
+ * (float [H][W][3], same layout, the pre-quantisation colour). */
+int pm_render(pm_scene* scene, const pm_render_params* params,
+              const pm_light* lights, int32_t num_lights,
+              const pm_photon_map* global_map, const pm_photon_map* caustic_map,
+              uint32_t* d_rgba, float* d_rgb, void* stream);
+typedef struct {
+  int64_t pixels, path_vertices, caustic_queries, global_queries, rays;
+} pm_render_stats;
+int pm_render_stats_get(pm_render_stats* out);
+
+/* ---- host-side boundary I/O (no GPU needed) ------------------------------ */
+/* config.toml (configLoader.h:8-19; keys of photon-mapping/src/hostCode.cu:153-158
+ * and ray-tracer/src/hostCode.cu:193-206). Strings are NUL-terminated. */
+typedef struct {
+  pm_float3 look_from, look_at, look_up; float fovy;
+  char photons_file[512], caustics_photons_file[512], model_path[512];
+  pm_float3 sky_colour; char output_filename[512];
+  int32_t fb_width, fb_height, samples_per_pixel, depth;
+  char viewer_output_filename[512], viewer_caustics_output_filename[512];
+  int32_t viewer_fb_width, viewer_fb_height;
+  int64_t casted_diffuse_photons, casted_caustics_photons; int32_t max_depth;
+  uint32_t present_mask;       /* bit i set = key i found (see pm_config_key_name) */
+  char error[512];
+} pm_config;
+int pm_config_load(const char* path, pm_config* out);
+const char* pm_config_key_name(int32_t i);
+
+/* Scene ingest (assetImporter.cxx:16-205): GLB (glTF 2.0 binary) or OBJ,
+ * BFS node flatten with node*parent transforms, per-mesh position dedup,
+ * <dir>/lights.txt, <stem>.mtl by material name; '/' and '\\' both accepted. */
+typedef struct pm_scene_data pm_scene_data;
+int pm_scene_data_load(const char* path, pm_scene_data** out);
+int pm_scene_data_counts(const pm_scene_data* s, int32_t* num_meshes,
+                         int32_t* num_lights, int64_t* num_vertices,
+                         int64_t* num_triangles);
+/* Borrowed views into the loaded scene (valid until pm_scene_data_free). */
+int pm_scene_data_meshes(const pm_scene_data* s, const pm_mesh** meshes);
+int pm_scene_data_lights(const pm_scene_data* s, const pm_light** lights);
+int pm_scene_data_mesh_name(const pm_scene_data* s, int32_t i, const char** name);
+int pm_scene_data_free(pm_scene_data* s);
+
+/* Photon text files (photon-mapping/src/hostCode.cu:31-49 writer, %.6f, 9
+ * values per line; ray-tracer/src/hostCode.cu:26-52 reader). */
+int pm_photons_write_txt(const char* path, const pm_photon* h_photons, int64_t n);
+int pm_photons_read_txt(const char* path, pm_photon** h_out, int64_t* n); /* free with pm_free */
+/* stbi_write_png(path, W, H, 4, rgba, W*4) (ray-tracer/src/hostCode.cu:240). */
+int pm_write_png_rgba(const char* path, const uint32_t* h_rgba, int32_t w, int32_t h);
+void pm_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PM_H_ */

@@ -1,0 +1,1078 @@
+/*
+ * pm_oracle.c — CPU ORACLE (test infrastructure only; see pm_oracle.h).
+ * Scalar C restatement of the reference photon-mapping hot path.
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off, no fast-math).
+ * PARITY UNPINNED against reference outputs (reference unbuildable here).
+ *
+ * Arithmetic spec shared with the HIP product: IEEE float32,
+ * round-to-nearest, no FMA contraction, correctly rounded / and sqrt, own
+ * polynomial acos/sin/cos, normalize(v) = v * (1/sqrt(dot(v,v))), watertight
+ * ray-triangle test, closest hit = argmin (t, global triangle index).
+ */
+#define _GNU_SOURCE
+#include "pm_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EPS 1e-3f                    /* common/cuda/helpers.h:8 */
+#define PI_F ((float)3.141592653)    /* helpers.h:9 */
+#define INFTY_F 1e10f                /* helpers.h:7 */
+#define PHOTON_TMAX 1e30f            /* owl::Ray default tmax (upstream OWL) */
+#define K_NEAREST 50                 /* ray-tracer/cuda/shading.h:7 */
+#define K_MAX_DISTANCE 100.0f        /* shading.h:8 */
+#define CONE_FILTER_C 1.1f           /* shading.h:9 */
+#define NUM_DIFFUSE_SAMPLES 20       /* ray-tracer/cuda/deviceCode.cu:15 */
+#define DIRECT_LIGHT_FACTOR 0.8f     /* deviceCode.cu:10 */
+#define CAUSTICS_FACTOR 0.08f        /* deviceCode.cu:11 */
+#define DIFFUSE_FACTOR 0.2f          /* deviceCode.cu:12 */
+
+enum { EV_MISS = 0, EV_ABSORBED = 1, EV_DIFFUSE = 2, EV_SPECULAR = 4, EV_REFRACT = 8 };
+
+/* ------------------------------------------------------------------------ */
+/* vec3 (owl::vec3f semantics, evaluation order left to right)               */
+typedef struct { float x, y, z; } v3;
+static inline v3 V3(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 add(v3 a, v3 b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 mulf(v3 a, float s) { return V3(a.x * s, a.y * s, a.z * s); }
+static inline v3 smul(float s, v3 a) { return V3(s * a.x, s * a.y, s * a.z); }
+static inline v3 mulv(v3 a, v3 b) { return V3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 divf(v3 a, float s) { return V3(a.x / s, a.y / s, a.z / s); }
+static inline v3 neg(v3 a) { return V3(-a.x, -a.y, -a.z); }
+static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 cross(v3 a, v3 b) {
+  return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+/* owl normalize = v * rsqrt(dot(v,v)); spec: rsqrt := 1/sqrtf */
+static inline v3 normalize(v3 v) { return mulf(v, 1.0f / sqrtf(dot(v, v))); }
+static inline float norm3(v3 v) { return sqrtf(dot(v, v)); }   /* helpers.h:23-25 */
+static inline v3 fromp(pm_float3 p) { return V3(p.x, p.y, p.z); }
+static inline pm_float3 top3(v3 v) { pm_float3 p = {v.x, v.y, v.z}; return p; }
+/* helpers.h:15-17 (signed test, kept) */
+static inline int near_zero(v3 v) { return v.x < EPS && v.y < EPS && v.z < EPS; }
+
+/* ------------------------------------------------------------------------ */
+/* owl::LCG<16> (upstream owl/common/math/random.h): TEA init + LCG draw.    */
+uint32_t orc_lcg_init(uint32_t val0, uint32_t val1) {
+  uint32_t v0 = val0, v1 = val1, s0 = 0;
+  for (int n = 0; n < 16; n++) {
+    s0 += 0x9e3779b9u;
+    v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + s0) ^ ((v1 >> 5) + 0xc8013ea4u);
+    v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + s0) ^ ((v0 >> 5) + 0x7e95761eu);
+  }
+  return v0;
+}
+float orc_lcg_next(uint32_t* state) {
+  *state = 1664525u * *state + 1013904223u;
+  return (float)(*state & 0x00FFFFFFu) / (float)0x01000000;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Deterministic trig (spec DESIGN.md §2; replaces CUDA acosf/sinf/cosf).    */
+float orc_acosf(float x) {
+  /* Abramowitz & Stegun 4.4.46 on |x|, reflected for x < 0. */
+  float ax = fabsf(x);
+  float p = -0.0012624911f;
+  p = p * ax + 0.0066700901f;
+  p = p * ax + -0.0170881256f;
+  p = p * ax + 0.0308918810f;
+  p = p * ax + -0.0501743046f;
+  p = p * ax + 0.0889789874f;
+  p = p * ax + -0.2145988016f;
+  p = p * ax + 1.5707963050f;
+  float r = sqrtf(1.0f - ax) * p;
+  return x < 0.0f ? 3.14159274f - r : r;
+}
+static void sincos_spec(float x, float* s, float* c) {
+  /* Cody-Waite reduction by pi/2 (3-part constant), cephes kernels. */
+  float q = rintf(x * 0.636619772f);
+  int k = (int)q;
+  float r = x - q * 1.5703125f;
+  r = r - q * 4.837512969970703125e-4f;
+  r = r - q * 7.549789954891882e-8f;
+  float r2 = r * r;
+  float sp = -1.9515295891e-4f;
+  sp = sp * r2 + 8.3321608736e-3f;
+  sp = sp * r2 + -1.6666654611e-1f;
+  sp = sp * r2;
+  sp = sp * r;
+  sp = sp + r;
+  float cp = 2.443315711809948e-5f;
+  cp = cp * r2 + -1.388731625493765e-3f;
+  cp = cp * r2 + 4.166664568298827e-2f;
+  cp = cp * (r2 * r2);
+  cp = (1.0f - 0.5f * r2) + cp;
+  switch (k & 3) {
+    case 0: *s = sp; *c = cp; break;
+    case 1: *s = cp; *c = -sp; break;
+    case 2: *s = -sp; *c = -cp; break;
+    default: *s = -cp; *c = sp; break;
+  }
+}
+float orc_sinf(float x) { float s, c; sincos_spec(x, &s, &c); return s; }
+float orc_cosf(float x) { float s, c; sincos_spec(x, &s, &c); return c; }
+
+/* helpers.h:27-34 randomPointInUnitSphere */
+static v3 random_point_in_unit_sphere(uint32_t* st) {
+  const float u = orc_lcg_next(st);
+  const float v = orc_lcg_next(st);
+  const float theta = 2.f * PI_F * u;
+  const float phi = orc_acosf(2.f * v - 1.f);
+  float sp, cp, st_, ct;
+  sincos_spec(phi, &sp, &cp);
+  sincos_spec(theta, &st_, &ct);
+  return V3(sp * ct, sp * st_, cp);
+}
+void orc_random_point_in_unit_sphere(uint32_t* state, float out[3]) {
+  v3 r = random_point_in_unit_sphere(state);
+  out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+/* helpers.h:36-43 randomUnitVector */
+static v3 random_unit_vector(uint32_t* st) {
+  v3 v;
+  do {
+    v.x = 2.f * orc_lcg_next(st) - 1.f;
+    v.y = 2.f * orc_lcg_next(st) - 1.f;
+    v.z = 2.f * orc_lcg_next(st) - 1.f;
+  } while (dot(v, v) >= 1.f);
+  return normalize(v);
+}
+/* helpers.h:45-47 */
+static v3 cosine_sample_hemisphere(v3 n, uint32_t* st) {
+  return normalize(add(n, mulf(random_point_in_unit_sphere(st), (1 - EPS))));
+}
+/* helpers.h:49-51 */
+static v3 reflect(v3 i, v3 n) { return sub(i, mulf(n, 2.f * dot(i, n))); }
+/* helpers.h:57-74 (normal not flipped on exit — kept) */
+static v3 refract_ior(v3 in, v3 n, float ior) {
+  float cos_theta = -dot(in, n);
+  float mu;
+  if (cos_theta > 0.f) {
+    mu = 1.f / ior;
+  } else {
+    mu = ior;
+    cos_theta = -cos_theta;
+  }
+  const float cos_phi = 1.f - mu * mu * (1.f - cos_theta * cos_theta);
+  if (cos_phi >= 0) return add(smul(mu, in), smul(mu * cos_theta - sqrtf(cos_phi), n));
+  return reflect(in, n);
+}
+void orc_refract(const float in[3], const float n[3], float ior, float out[3]) {
+  v3 r = refract_ior(V3(in[0], in[1], in[2]), V3(n[0], n[1], n[2]), ior);
+  out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+/* helpers.h:91-106 refract(v, n, ni_over_nt, &refracted) */
+static int refract_uv(v3 v, v3 n, float ni, v3* refracted) {
+  const v3 uv = normalize(v);
+  const float dt = dot(uv, n);
+  const float disc = 1.0f - ni * ni * (1 - dt * dt);
+  if (disc > 0.f) {
+    *refracted = sub(smul(ni, sub(uv, mulf(n, dt))), mulf(n, sqrtf(disc)));
+    return 1;
+  }
+  return 0;
+}
+/* helpers.h:108-112: double arithmetic; pow(x,5) := ((x*x)*(x*x))*x */
+static float schlick(float cosv, float ior) {
+  float r0 = (float)((1. - (double)ior) / (1. + (double)ior));
+  r0 = r0 * r0;
+  double x = 1. - (double)cosv;
+  double x2 = x * x;
+  double p5 = (x2 * x2) * x;
+  return (float)((double)r0 + (1. - (double)r0) * p5);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Scene: triangles + optional own BVH (conservative culling).               */
+typedef struct { float lo[3], hi[3]; int32_t left, count; } onode;
+struct orc_scene {
+  int64_t ntri;
+  float* tri;          /* ntri * 9: A, B, C world-space */
+  int32_t* mesh;
+  int32_t* prim;
+  pm_material* mat;
+  int32_t nmesh;
+  int use_bvh;
+  onode* nodes;
+  int32_t nnodes;
+  int32_t* order;
+  float pad;
+};
+
+typedef struct {
+  v3 o, d, inv;
+  int kx, ky, kz;
+  float Sx, Sy, Sz;
+} rayp;
+
+static void ray_prep(rayp* r, v3 o, v3 d) {
+  r->o = o; r->d = d;
+  float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+  int kz = ax > ay ? (ax > az ? 0 : 2) : (ay > az ? 1 : 2);
+  int kx = kz + 1; if (kx == 3) kx = 0;
+  int ky = kx + 1; if (ky == 3) ky = 0;
+  float dd[3] = {d.x, d.y, d.z};
+  if (dd[kz] < 0.0f) { int t = kx; kx = ky; ky = t; }
+  r->kx = kx; r->ky = ky; r->kz = kz;
+  r->Sx = dd[kx] / dd[kz];
+  r->Sy = dd[ky] / dd[kz];
+  r->Sz = 1.0f / dd[kz];
+  float iv[3];
+  for (int i = 0; i < 3; i++) {
+    float c = dd[i];
+    if (fabsf(c) < 1e-20f) c = copysignf(1e-20f, c);
+    iv[i] = 1.0f / c;
+  }
+  r->inv = V3(iv[0], iv[1], iv[2]);
+}
+
+/* Watertight ray/triangle (Woop, Benthin, Wald 2013) — stands in for the
+ * OptiX built-in triangle test used by every optixTrace/owl::traceRay call. */
+static int wt_hit(const float* t9, const rayp* r, float* tout) {
+  const float oo[3] = {r->o.x, r->o.y, r->o.z};
+  float A[3], B[3], C[3];
+  for (int i = 0; i < 3; i++) {
+    A[i] = t9[i] - oo[i];
+    B[i] = t9[3 + i] - oo[i];
+    C[i] = t9[6 + i] - oo[i];
+  }
+  const int kx = r->kx, ky = r->ky, kz = r->kz;
+  const float Ax = A[kx] - r->Sx * A[kz], Ay = A[ky] - r->Sy * A[kz];
+  const float Bx = B[kx] - r->Sx * B[kz], By = B[ky] - r->Sy * B[kz];
+  const float Cx = C[kx] - r->Sx * C[kz], Cy = C[ky] - r->Sy * C[kz];
+  float U = Cx * By - Cy * Bx;
+  float Vv = Ax * Cy - Ay * Cx;
+  float W = Bx * Ay - By * Ax;
+  if (U == 0.0f || Vv == 0.0f || W == 0.0f) {
+    double CxBy = (double)Cx * (double)By, CyBx = (double)Cy * (double)Bx;
+    U = (float)(CxBy - CyBx);
+    double AxCy = (double)Ax * (double)Cy, AyCx = (double)Ay * (double)Cx;
+    Vv = (float)(AxCy - AyCx);
+    double BxAy = (double)Bx * (double)Ay, ByAx = (double)By * (double)Ax;
+    W = (float)(BxAy - ByAx);
+  }
+  if ((U < 0.0f || Vv < 0.0f || W < 0.0f) && (U > 0.0f || Vv > 0.0f || W > 0.0f)) return 0;
+  const float det = U + Vv + W;
+  if (det == 0.0f) return 0;
+  const float Az = r->Sz * A[kz], Bz = r->Sz * B[kz], Cz = r->Sz * C[kz];
+  const float T = U * Az + Vv * Bz + W * Cz;
+  *tout = T / det;
+  return 1;
+}
+
+static int box_hit(const onode* n, const rayp* r, float tmin, float tmax) {
+  float t0x = (n->lo[0] - r->o.x) * r->inv.x, t1x = (n->hi[0] - r->o.x) * r->inv.x;
+  float t0y = (n->lo[1] - r->o.y) * r->inv.y, t1y = (n->hi[1] - r->o.y) * r->inv.y;
+  float t0z = (n->lo[2] - r->o.z) * r->inv.z, t1z = (n->hi[2] - r->o.z) * r->inv.z;
+  float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+  float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
+  return tn <= tf;
+}
+
+static int cmp_axis;
+static const float* cmp_cent;
+static int cmp_idx(const void* a, const void* b) {
+  int ia = *(const int32_t*)a, ib = *(const int32_t*)b;
+  float ca = cmp_cent[ia * 3 + cmp_axis], cb = cmp_cent[ib * 3 + cmp_axis];
+  if (ca < cb) return -1;
+  if (ca > cb) return 1;
+  return ia < ib ? -1 : (ia > ib);
+}
+
+static int32_t bvh_build_rec(orc_scene* s, const float* cent, int32_t lo, int32_t hi) {
+  int32_t id = s->nnodes++;
+  onode* n = &s->nodes[id];
+  for (int k = 0; k < 3; k++) { n->lo[k] = FLT_MAX; n->hi[k] = -FLT_MAX; }
+  for (int32_t i = lo; i < hi; i++) {
+    const float* t = &s->tri[(int64_t)s->order[i] * 9];
+    for (int v = 0; v < 3; v++)
+      for (int k = 0; k < 3; k++) {
+        n->lo[k] = fminf(n->lo[k], t[v * 3 + k]);
+        n->hi[k] = fmaxf(n->hi[k], t[v * 3 + k]);
+      }
+  }
+  for (int k = 0; k < 3; k++) { n->lo[k] -= s->pad; n->hi[k] += s->pad; }
+  if (hi - lo <= 4) {
+    n->left = lo;
+    n->count = hi - lo;
+    return id;
+  }
+  float ext[3];
+  for (int k = 0; k < 3; k++) ext[k] = n->hi[k] - n->lo[k];
+  cmp_axis = ext[0] > ext[1] ? (ext[0] > ext[2] ? 0 : 2) : (ext[1] > ext[2] ? 1 : 2);
+  cmp_cent = cent;
+  qsort(&s->order[lo], (size_t)(hi - lo), sizeof(int32_t), cmp_idx);
+  int32_t mid = lo + (hi - lo) / 2;
+  n->count = 0;
+  bvh_build_rec(s, cent, lo, mid);                       /* left = id + 1 */
+  int32_t right = bvh_build_rec(s, cent, mid, hi);
+  s->nodes[id].left = right;
+  return id;
+}
+
+int orc_scene_create(const pm_mesh* meshes, int32_t nm, int32_t use_bvh, orc_scene** out) {
+  if (!out || nm < 0) return PM_ERR_INVALID;
+  orc_scene* s = (orc_scene*)calloc(1, sizeof(orc_scene));
+  int64_t nt = 0;
+  for (int i = 0; i < nm; i++) nt += meshes[i].num_triangles;
+  s->ntri = nt;
+  s->nmesh = nm;
+  s->tri = (float*)malloc(sizeof(float) * 9 * (size_t)(nt > 0 ? nt : 1));
+  s->mesh = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nt > 0 ? nt : 1));
+  s->prim = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nt > 0 ? nt : 1));
+  s->mat = (pm_material*)malloc(sizeof(pm_material) * (size_t)(nm > 0 ? nm : 1));
+  float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  int64_t t = 0;
+  for (int m = 0; m < nm; m++) {
+    s->mat[m] = meshes[m].material;
+    for (int j = 0; j < meshes[m].num_triangles; j++, t++) {
+      const pm_int3 ix = meshes[m].indices[j];
+      const int32_t id3[3] = {ix.x, ix.y, ix.z};
+      for (int v = 0; v < 3; v++) {
+        if (id3[v] < 0 || id3[v] >= meshes[m].num_vertices) { orc_scene_destroy(s); return PM_ERR_INVALID; }
+        pm_float3 p = meshes[m].vertices[id3[v]];
+        s->tri[t * 9 + v * 3 + 0] = p.x;
+        s->tri[t * 9 + v * 3 + 1] = p.y;
+        s->tri[t * 9 + v * 3 + 2] = p.z;
+        lo[0] = fminf(lo[0], p.x); lo[1] = fminf(lo[1], p.y); lo[2] = fminf(lo[2], p.z);
+        hi[0] = fmaxf(hi[0], p.x); hi[1] = fmaxf(hi[1], p.y); hi[2] = fmaxf(hi[2], p.z);
+      }
+      s->mesh[t] = m;
+      s->prim[t] = j;
+    }
+  }
+  float ext = 0.f;
+  for (int k = 0; k < 3; k++) if (nt > 0) ext = fmaxf(ext, hi[k] - lo[k]);
+  s->pad = ext * 1e-5f + 1e-20f;
+  s->use_bvh = use_bvh && nt > 0;
+  if (s->use_bvh) {
+    float* cent = (float*)malloc(sizeof(float) * 3 * (size_t)nt);
+    for (int64_t i = 0; i < nt; i++)
+      for (int k = 0; k < 3; k++)
+        cent[i * 3 + k] = (s->tri[i * 9 + k] + s->tri[i * 9 + 3 + k] + s->tri[i * 9 + 6 + k]) / 3.0f;
+    s->order = (int32_t*)malloc(sizeof(int32_t) * (size_t)nt);
+    for (int64_t i = 0; i < nt; i++) s->order[i] = (int32_t)i;
+    s->nodes = (onode*)malloc(sizeof(onode) * (size_t)(2 * nt + 1));
+    s->nnodes = 0;
+    bvh_build_rec(s, cent, 0, (int32_t)nt);
+    free(cent);
+  }
+  *out = s;
+  return PM_OK;
+}
+
+void orc_scene_destroy(orc_scene* s) {
+  if (!s) return;
+  free(s->tri); free(s->mesh); free(s->prim); free(s->mat);
+  free(s->nodes); free(s->order);
+  free(s);
+}
+int64_t orc_scene_num_triangles(const orc_scene* s) { return s->ntri; }
+
+/* closest hit in (tmin, tmax): argmin (t, triangle index). Returns tri or -1. */
+static int64_t closest_hit(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, float* tbest) {
+  rayp r;
+  ray_prep(&r, o, d);
+  float bt = tmax;
+  int64_t bid = -1;
+  if (!s->use_bvh) {
+    for (int64_t i = 0; i < s->ntri; i++) {
+      float t;
+      if (!wt_hit(&s->tri[i * 9], &r, &t)) continue;
+      if (!(t > tmin && t < tmax)) continue;
+      if (bid < 0 || t < bt || (t == bt && i < bid)) { bt = t; bid = i; }
+    }
+  } else {
+    int32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+      const onode* n = &s->nodes[stack[--sp]];
+      float lim = bid < 0 ? tmax : bt * 1.00001f;
+      if (!box_hit(n, &r, tmin, lim)) continue;
+      if (n->count > 0) {
+        for (int32_t j = 0; j < n->count; j++) {
+          int64_t i = s->order[n->left + j];
+          float t;
+          if (!wt_hit(&s->tri[i * 9], &r, &t)) continue;
+          if (!(t > tmin && t < tmax)) continue;
+          if (bid < 0 || t < bt || (t == bt && i < bid)) { bt = t; bid = i; }
+        }
+      } else {
+        int32_t self = (int32_t)(n - s->nodes);
+        stack[sp++] = n->left;
+        stack[sp++] = self + 1;
+      }
+    }
+  }
+  *tbest = bt;
+  return bid;
+}
+
+static int any_hit(const orc_scene* s, v3 o, v3 d, float tmin, float tmax) {
+  rayp r;
+  ray_prep(&r, o, d);
+  if (!s->use_bvh) {
+    for (int64_t i = 0; i < s->ntri; i++) {
+      float t;
+      if (wt_hit(&s->tri[i * 9], &r, &t) && t > tmin && t < tmax) return 1;
+    }
+    return 0;
+  }
+  int32_t stack[128];
+  int sp = 0;
+  stack[sp++] = 0;
+  while (sp) {
+    const onode* n = &s->nodes[stack[--sp]];
+    if (!box_hit(n, &r, tmin, tmax * 1.00001f)) continue;
+    if (n->count > 0) {
+      for (int32_t j = 0; j < n->count; j++) {
+        int64_t i = s->order[n->left + j];
+        float t;
+        if (wt_hit(&s->tri[i * 9], &r, &t) && t > tmin && t < tmax) return 1;
+      }
+    } else {
+      int32_t self = (int32_t)(n - s->nodes);
+      stack[sp++] = n->left;
+      stack[sp++] = self + 1;
+    }
+  }
+  return 0;
+}
+
+int orc_intersect(const orc_scene* s, const pm_ray* rays, int64_t n, pm_hit* hits) {
+  for (int64_t i = 0; i < n; i++) {
+    float t;
+    int64_t id = closest_hit(s, fromp(rays[i].origin), fromp(rays[i].direction),
+                             rays[i].tmin, rays[i].tmax, &t);
+    if (id < 0) {
+      hits[i].t = INFINITY; hits[i].mesh = -1; hits[i].prim = -1; hits[i].tri = -1;
+    } else {
+      hits[i].t = t; hits[i].mesh = s->mesh[id]; hits[i].prim = s->prim[id]; hits[i].tri = (int32_t)id;
+    }
+  }
+  return PM_OK;
+}
+int orc_occluded(const orc_scene* s, const pm_ray* rays, int64_t n, int32_t* occ) {
+  for (int64_t i = 0; i < n; i++)
+    occ[i] = any_hit(s, fromp(rays[i].origin), fromp(rays[i].direction), rays[i].tmin, rays[i].tmax);
+  return PM_OK;
+}
+
+/* helpers.h:76-85 getPrimitiveNormal (unflipped geometric normal) */
+static v3 prim_normal(const orc_scene* s, int64_t tri) {
+  const float* t = &s->tri[tri * 9];
+  v3 A = V3(t[0], t[1], t[2]), B = V3(t[3], t[4], t[5]), C = V3(t[6], t[7], t[8]);
+  return normalize(cross(sub(B, A), sub(C, A)));
+}
+
+/* ------------------------------------------------------------------------ */
+/* tiny parallel-for                                                          */
+typedef void (*pf_fn)(void* ctx, int64_t lo, int64_t hi);
+typedef struct { pf_fn fn; void* ctx; int64_t n, chunk; int64_t next; pthread_mutex_t mu; } pf_t;
+static void* pf_worker(void* a) {
+  pf_t* p = (pf_t*)a;
+  for (;;) {
+    pthread_mutex_lock(&p->mu);
+    int64_t lo = p->next;
+    p->next += p->chunk;
+    pthread_mutex_unlock(&p->mu);
+    if (lo >= p->n) break;
+    int64_t hi = lo + p->chunk < p->n ? lo + p->chunk : p->n;
+    p->fn(p->ctx, lo, hi);
+  }
+  return NULL;
+}
+static void parallel_for(int64_t n, int64_t chunk, int nthreads, pf_fn fn, void* ctx) {
+  if (n <= 0) return;
+  if (nthreads <= 1) { fn(ctx, 0, n); return; }
+  pf_t p;
+  p.fn = fn; p.ctx = ctx; p.n = n; p.chunk = chunk > 0 ? chunk : 1; p.next = 0;
+  pthread_mutex_init(&p.mu, NULL);
+  pthread_t th[256];
+  if (nthreads > 256) nthreads = 256;
+  for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, pf_worker, &p);
+  for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+  pthread_mutex_destroy(&p.mu);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Stage 1: photon tracer                                                     */
+/* photon-mapping/src/hostCode.cu:102-110 + :86 */
+int orc_photons_per_light(const pm_light* lights, int32_t nl, int64_t casted, int64_t* counts) {
+  double total = 0;
+  for (int i = 0; i < nl; i++) total += lights[i].power;
+  if (!(total > 0.0)) { for (int i = 0; i < nl; i++) counts[i] = 0; return PM_OK; }
+  int ppw = (int)((double)(int)casted / total);
+  for (int i = 0; i < nl; i++) counts[i] = (int64_t)(int)(lights[i].power * ppw);
+  return PM_OK;
+}
+
+typedef struct {
+  const orc_scene* s;
+  const pm_light* lights;
+  int32_t nl;
+  const int64_t* loff;   /* nl+1 prefix of per-light counts */
+  int64_t g_lo;
+  int32_t maxd, caustic;
+  pm_photon* slots;      /* [g - g_lo][maxd] */
+  uint8_t* cnt;
+} trace_ctx;
+
+/* photon-mapping/cuda/deviceCode.cu:54-72 (raygen) + :25-52 (bounce loops)
+ * + :113-131 (closest hit) + :74-111 (scatter) + :10-17 (deposit). */
+static void trace_one(const trace_ctx* c, int64_t g) {
+  int l = 0;
+  while (g >= c->loff[l + 1]) l++;
+  const uint32_t id = (uint32_t)(g - c->loff[l]);
+  const pm_light* L = &c->lights[l];
+  uint32_t rng = orc_lcg_init(id, 0);
+  v3 color = fromp(L->rgb);
+  v3 o = fromp(L->pos);
+  v3 d = random_point_in_unit_sphere(&rng);
+  const float tmin = EPS;
+  pm_photon* out = &c->slots[(g - c->g_lo) * c->maxd];
+  int n = 0;
+  for (int i = 0; i < c->maxd; i++) {
+    float t;
+    int64_t tri = closest_hit(c->s, o, d, tmin, PHOTON_TMAX, &t);
+    int ev;
+    v3 so = {0, 0, 0}, sd = {0, 0, 0}, sc = {0, 0, 0};
+    if (tri < 0) {
+      ev = EV_MISS;
+    } else {
+      const pm_material* m = &c->s->mat[c->s->mesh[tri]];
+      const float pd = m->diffuse;
+      const float ps = m->specular + pd;
+      const float pt = m->transmission + ps;
+      const float rp = orc_lcg_next(&rng);
+      const v3 hp = add(o, smul(t, d));
+      const v3 albedo = fromp(m->albedo);
+      if (rp < pd) {
+        ev = EV_DIFFUSE;
+        so = hp;
+        sd = cosine_sample_hemisphere(prim_normal(c->s, tri), &rng);
+        sc = mulv(albedo, color);
+      } else if (rp < ps) {
+        ev = EV_SPECULAR;
+        so = hp;
+        sd = reflect(d, prim_normal(c->s, tri));
+        sc = mulv(albedo, color);
+      } else if (rp < pt) {
+        ev = EV_REFRACT;
+        so = hp;
+        sd = refract_ior(d, prim_normal(c->s, tri), m->refraction_idx);
+        sc = mulv(albedo, color);
+      } else {
+        ev = EV_ABSORBED;
+      }
+    }
+    if (!c->caustic) {
+      if (ev == EV_DIFFUSE) {
+        if (i > 0) {
+          pm_photon* p = &out[n++];
+          p->pos = top3(so); p->dir = top3(sd); p->power = 0; p->color = top3(color);
+        }
+        o = so; d = sd; color = sc;
+      } else {
+        break;
+      }
+    } else {
+      if (i > 0 && ev == EV_DIFFUSE) {
+        pm_photon* p = &out[n++];
+        p->pos = top3(so); p->dir = top3(sd); p->power = 0; p->color = top3(color);
+      }
+      if (ev & (EV_SPECULAR | EV_REFRACT)) {
+        o = so; d = sd; color = sc;
+      } else {
+        break;
+      }
+    }
+  }
+  c->cnt[g - c->g_lo] = (uint8_t)n;
+}
+static void trace_range(void* ctx, int64_t lo, int64_t hi) {
+  const trace_ctx* c = (const trace_ctx*)ctx;
+  for (int64_t i = lo; i < hi; i++) trace_one(c, c->g_lo + i);
+}
+
+int orc_trace_photon_range(const orc_scene* s, const pm_light* lights, int32_t nl,
+                           const pm_trace_params* p, int64_t g_lo, int64_t g_hi,
+                           int32_t nthreads, pm_photon* out, int64_t capacity, int64_t* count) {
+  if (!s || !p || !count || nl < 0 || p->max_depth < 0 || p->max_depth > 255) return PM_ERR_INVALID;
+  int64_t* cnts = (int64_t*)calloc((size_t)nl + 1, sizeof(int64_t));
+  int64_t* loff = (int64_t*)calloc((size_t)nl + 2, sizeof(int64_t));
+  orc_photons_per_light(lights, nl, p->casted_photons, cnts);
+  for (int i = 0; i < nl; i++) loff[i + 1] = loff[i] + (cnts[i] > 0 ? cnts[i] : 0);
+  loff[nl + 1] = INT64_MAX;
+  if (g_hi > loff[nl]) g_hi = loff[nl];
+  if (g_lo < 0) g_lo = 0;
+  int64_t np = g_hi > g_lo ? g_hi - g_lo : 0;
+  int maxd = p->max_depth;
+  trace_ctx c;
+  c.s = s; c.lights = lights; c.nl = nl; c.loff = loff; c.g_lo = g_lo;
+  c.maxd = maxd; c.caustic = p->caustics_mode;
+  c.slots = (pm_photon*)malloc(sizeof(pm_photon) * (size_t)(np * (maxd > 0 ? maxd : 1) + 1));
+  c.cnt = (uint8_t*)calloc((size_t)np + 1, 1);
+  parallel_for(np, 256, nthreads, trace_range, &c);
+  int64_t total = 0;
+  for (int64_t i = 0; i < np; i++) total += c.cnt[i];
+  *count = total;
+  int st = PM_OK;
+  if (total > capacity || (total > 0 && !out)) {
+    st = PM_ERR_CAPACITY;
+  } else {
+    int64_t w = 0;
+    for (int64_t i = 0; i < np; i++)
+      for (int j = 0; j < c.cnt[i]; j++) out[w++] = c.slots[i * maxd + j];
+  }
+  free(c.slots); free(c.cnt); free(cnts); free(loff);
+  return st;
+}
+
+int orc_trace_photons(const orc_scene* s, const pm_light* lights, int32_t nl,
+                      const pm_trace_params* p, int32_t nthreads,
+                      pm_photon* out, int64_t capacity, int64_t* count) {
+  if (!p || p->shard_count < 1 || p->shard_rank < 0 || p->shard_rank >= p->shard_count)
+    return PM_ERR_INVALID;
+  int64_t* cnts = (int64_t*)calloc((size_t)nl + 1, sizeof(int64_t));
+  orc_photons_per_light(lights, nl, p->casted_photons, cnts);
+  int64_t tot = 0;
+  for (int i = 0; i < nl; i++) tot += cnts[i] > 0 ? cnts[i] : 0;
+  free(cnts);
+  int64_t lo = tot * p->shard_rank / p->shard_count;
+  int64_t hi = tot * (p->shard_rank + 1) / p->shard_count;
+  return orc_trace_photon_range(s, lights, nl, p, lo, hi, nthreads, out, capacity, count);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Stage 2: photon map (own kd-tree, exact kNN by (d^2, original index))      */
+struct orc_map {
+  int64_t n;
+  float* pos;      /* n*3 */
+  float* col;      /* n*3 */
+  float* pw;       /* n   */
+  int32_t* idx;    /* kd order -> original index */
+  int32_t* node_lo; int32_t* node_hi; int8_t* node_dim; float* node_split; int32_t nnodes;
+};
+
+/* ray-tracer/src/hostCode.cu:54-83 loadPhotons: map = a (power_a) ++ b (power_b) */
+static int ocmp_dim;
+static const float* ocmp_pos;
+static int ocmp(const void* a, const void* b) {
+  int32_t ia = *(const int32_t*)a, ib = *(const int32_t*)b;
+  float ca = ocmp_pos[(int64_t)ia * 3 + ocmp_dim], cb = ocmp_pos[(int64_t)ib * 3 + ocmp_dim];
+  if (ca < cb) return -1;
+  if (ca > cb) return 1;
+  return ia < ib ? -1 : (ia > ib);
+}
+/* Node layout: implicit binary tree over the idx array, leaves <= 8 points. */
+static void kd_build(orc_map* m, int32_t node, int64_t lo, int64_t hi) {
+  m->node_lo[node] = (int32_t)lo;
+  m->node_hi[node] = (int32_t)hi;
+  if (hi - lo <= 8 || 2 * node + 2 >= m->nnodes) { m->node_dim[node] = -1; return; }
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int64_t i = lo; i < hi; i++)
+    for (int k = 0; k < 3; k++) {
+      float v = m->pos[(int64_t)m->idx[i] * 3 + k];
+      mn[k] = fminf(mn[k], v); mx[k] = fmaxf(mx[k], v);
+    }
+  int dim = 0;
+  for (int k = 1; k < 3; k++) if (mx[k] - mn[k] > mx[dim] - mn[dim]) dim = k;
+  ocmp_dim = dim; ocmp_pos = m->pos;
+  qsort(&m->idx[lo], (size_t)(hi - lo), sizeof(int32_t), ocmp);
+  int64_t mid = lo + (hi - lo) / 2;
+  m->node_dim[node] = (int8_t)dim;
+  m->node_split[node] = m->pos[(int64_t)m->idx[mid] * 3 + dim];
+  kd_build(m, 2 * node + 1, lo, mid);
+  kd_build(m, 2 * node + 2, mid, hi);
+}
+
+int orc_map_create(const pm_photon* a, int64_t na, float power_a,
+                   const pm_photon* b, int64_t nb, float power_b, orc_map** out) {
+  if (!out || na < 0 || nb < 0) return PM_ERR_INVALID;
+  orc_map* m = (orc_map*)calloc(1, sizeof(orc_map));
+  int64_t n = na + nb;
+  m->n = n;
+  m->pos = (float*)malloc(sizeof(float) * 3 * (size_t)(n + 1));
+  m->col = (float*)malloc(sizeof(float) * 3 * (size_t)(n + 1));
+  m->pw = (float*)malloc(sizeof(float) * (size_t)(n + 1));
+  m->idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1));
+  for (int64_t i = 0; i < n; i++) {
+    const pm_photon* p = i < na ? &a[i] : &b[i - na];
+    m->pos[i * 3 + 0] = p->pos.x; m->pos[i * 3 + 1] = p->pos.y; m->pos[i * 3 + 2] = p->pos.z;
+    m->col[i * 3 + 0] = p->color.x; m->col[i * 3 + 1] = p->color.y; m->col[i * 3 + 2] = p->color.z;
+    m->pw[i] = i < na ? power_a : power_b;
+    m->idx[i] = (int32_t)i;
+  }
+  int32_t nn = 1;
+  while ((int64_t)nn * 8 < n * 2 && nn < (1 << 26)) nn *= 2;
+  m->nnodes = 2 * nn;
+  m->node_lo = (int32_t*)calloc((size_t)m->nnodes, sizeof(int32_t));
+  m->node_hi = (int32_t*)calloc((size_t)m->nnodes, sizeof(int32_t));
+  m->node_dim = (int8_t*)calloc((size_t)m->nnodes, sizeof(int8_t));
+  m->node_split = (float*)calloc((size_t)m->nnodes, sizeof(float));
+  kd_build(m, 0, 0, n);
+  *out = m;
+  return PM_OK;
+}
+void orc_map_destroy(orc_map* m) {
+  if (!m) return;
+  free(m->pos); free(m->col); free(m->pw); free(m->idx);
+  free(m->node_lo); free(m->node_hi); free(m->node_dim); free(m->node_split);
+  free(m);
+}
+
+typedef struct { float d2; int32_t id; } cand;
+static inline int cand_less(cand a, cand b) { return a.d2 < b.d2 || (a.d2 == b.d2 && a.id < b.id); }
+typedef struct { cand* h; int k, cnt; float r2; } heap_t;
+static void heap_push(heap_t* H, cand c) {
+  if (!(c.d2 < H->r2)) return;
+  if (H->cnt < H->k) {
+    int i = H->cnt++;
+    H->h[i] = c;
+    while (i > 0) {
+      int p = (i - 1) / 2;
+      if (cand_less(H->h[p], H->h[i])) { cand t = H->h[p]; H->h[p] = H->h[i]; H->h[i] = t; i = p; }
+      else break;
+    }
+    return;
+  }
+  if (!cand_less(c, H->h[0])) return;
+  H->h[0] = c;
+  int i = 0;
+  for (;;) {
+    int l = 2 * i + 1, r = l + 1, b = i;
+    if (l < H->k && cand_less(H->h[b], H->h[l])) b = l;
+    if (r < H->k && cand_less(H->h[b], H->h[r])) b = r;
+    if (b == i) break;
+    cand t = H->h[b]; H->h[b] = H->h[i]; H->h[i] = t; i = b;
+  }
+}
+static inline float heap_bound(const heap_t* H) { return H->cnt < H->k ? H->r2 : H->h[0].d2; }
+
+static void knn_rec(const orc_map* m, int32_t node, const float q[3], heap_t* H) {
+  if (m->node_dim[node] < 0) {
+    for (int32_t i = m->node_lo[node]; i < m->node_hi[node]; i++) {
+      int32_t pid = m->idx[i];
+      const float* p = &m->pos[(int64_t)pid * 3];
+      /* cukd sqrDistance == dot(q - p, q - p) */
+      float dx = q[0] - p[0], dy = q[1] - p[1], dz = q[2] - p[2];
+      cand c = {dx * dx + dy * dy + dz * dz, pid};
+      heap_push(H, c);
+    }
+    return;
+  }
+  int dim = m->node_dim[node];
+  float diff = q[dim] - m->node_split[node];
+  int32_t nearc = diff < 0.f ? 2 * node + 1 : 2 * node + 2;
+  int32_t farc = diff < 0.f ? 2 * node + 2 : 2 * node + 1;
+  knn_rec(m, nearc, q, H);
+  if (diff * diff <= heap_bound(H)) knn_rec(m, farc, q, H);
+}
+static int cmp_cand(const void* a, const void* b) {
+  cand x = *(const cand*)a, y = *(const cand*)b;
+  return cand_less(x, y) ? -1 : (cand_less(y, x) ? 1 : 0);
+}
+/* k nearest, sorted ascending by (d2, id); returns max d2 (radius^2 if not full) */
+static float knn_one(const orc_map* m, const float q[3], int k, float radius, cand* buf) {
+  heap_t H = {buf, k, 0, radius * radius};
+  if (m->n > 0) knn_rec(m, 0, q, &H);
+  float r2 = heap_bound(&H);
+  qsort(buf, (size_t)H.cnt, sizeof(cand), cmp_cand);
+  for (int i = H.cnt; i < k; i++) { buf[i].d2 = H.r2; buf[i].id = -1; }
+  return r2;
+}
+
+typedef struct {
+  const orc_map* m; const pm_float3* q; int k; float radius;
+  int32_t* ids; float* d2; float* maxd2;
+} knn_ctx;
+static void knn_range(void* vc, int64_t lo, int64_t hi) {
+  knn_ctx* c = (knn_ctx*)vc;
+  cand* buf = (cand*)malloc(sizeof(cand) * (size_t)c->k);
+  for (int64_t i = lo; i < hi; i++) {
+    float q[3] = {c->q[i].x, c->q[i].y, c->q[i].z};
+    float r2 = knn_one(c->m, q, c->k, c->radius, buf);
+    for (int j = 0; j < c->k; j++) {
+      c->ids[i * c->k + j] = buf[j].id;
+      if (c->d2) c->d2[i * c->k + j] = buf[j].d2;
+    }
+    if (c->maxd2) c->maxd2[i] = r2;
+  }
+  free(buf);
+}
+int orc_knn(const orc_map* m, const pm_float3* q, int64_t nq, int32_t k, float max_radius,
+            int32_t nthreads, int32_t* ids, float* d2, float* maxd2) {
+  if (!m || k < 1 || k > 256) return PM_ERR_INVALID;
+  knn_ctx c = {m, q, k, max_radius, ids, d2, maxd2};
+  parallel_for(nq, 256, nthreads, knn_range, &c);
+  return PM_OK;
+}
+
+/* shading.h:93-121 gatherPhotons; sum in (d^2, id) order */
+static v3 gather_one(const orc_map* m, v3 hit, float brdf, cand* buf) {
+  float q[3] = {hit.x, hit.y, hit.z};
+  const float r2 = knn_one(m, q, K_NEAREST, K_MAX_DISTANCE, buf);
+  v3 flux = V3(0.f, 0.f, 0.f);
+  for (int p = 0; p < K_NEAREST; p++) {
+    const int32_t id = buf[p].id;
+    if (id < 0 || id > m->n) continue;
+    const float power = m->pw[id];
+    const v3 ppos = V3(m->pos[(int64_t)id * 3], m->pos[(int64_t)id * 3 + 1], m->pos[(int64_t)id * 3 + 2]);
+    const v3 pcol = V3(m->col[(int64_t)id * 3], m->col[(int64_t)id * 3 + 1], m->col[(int64_t)id * 3 + 2]);
+    const float dist = norm3(sub(ppos, hit));
+    const float w = 1 - (dist / sqrtf(r2) * CONE_FILTER_C);
+    flux = add(flux, smul(brdf * power * w, pcol));
+  }
+  return divf(flux, (1 - (2.f / 3.f) * (1.f / CONE_FILTER_C)) * 2 * PI_F * r2);
+}
+typedef struct { const orc_map* m; const pm_float3* p; const float* brdf; pm_float3* out; } gather_ctx;
+static void gather_range(void* vc, int64_t lo, int64_t hi) {
+  gather_ctx* c = (gather_ctx*)vc;
+  cand buf[K_NEAREST];
+  for (int64_t i = lo; i < hi; i++) c->out[i] = top3(gather_one(c->m, fromp(c->p[i]), c->brdf[i], buf));
+}
+int orc_gather(const orc_map* m, const pm_float3* pts, const float* brdf, int64_t nq,
+               int32_t nthreads, pm_float3* out) {
+  gather_ctx c = {m, pts, brdf, out};
+  parallel_for(nq, 256, nthreads, gather_range, &c);
+  return PM_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Render (ray-tracer/cuda/deviceCode.cu:25-231, shading.h:20-91)             */
+int orc_camera_setup(pm_float3 look_from, pm_float3 look_at, pm_float3 look_up, float fovy,
+                     int32_t w, int32_t h, pm_camera* out) {
+  /* ray-tracer/src/hostCode.cu:100-108 (cos, not tan, kept) */
+  const float aspect = (float)w / (float)h;
+  const float cosf_ = cosf(fovy);
+  v3 from = fromp(look_from), at = fromp(look_at), up = fromp(look_up);
+  v3 d00 = normalize(sub(at, from));
+  v3 du = smul(cosf_ * aspect, normalize(cross(d00, up)));
+  v3 dv = smul(cosf_, normalize(cross(du, d00)));
+  d00 = sub(d00, smul(0.5f, add(du, dv)));
+  out->pos = top3(from); out->dir_00 = top3(d00); out->dir_du = top3(du); out->dir_dv = top3(dv);
+  return PM_OK;
+}
+
+typedef struct { v3 hitpoint, normal; pm_material mat; } hitrec;
+typedef struct { uint32_t rng; v3 colour; int missed; hitrec hr; } prd_t;
+
+/* closestHit (deviceCode.cu:233-253) */
+static void trace_closest(const orc_scene* s, v3 o, v3 d, float tmin, float tmax, hitrec* hr, int* missed,
+                          pm_render_stats* st) {
+  float t;
+  int64_t tri = closest_hit(s, o, d, tmin, tmax, &t);
+  if (st) st->rays++;
+  if (tri < 0) { *missed = 1; return; }
+  hr->mat = s->mat[s->mesh[tri]];
+  hr->hitpoint = add(o, mulf(d, t));
+  const v3 n = prim_normal(s, tri);
+  hr->normal = dot(d, n) < 0.f ? n : neg(n);
+  hr->normal = normalize(hr->normal);
+  *missed = 0;
+}
+
+/* shading.h:82-91 */
+static float specular_brdf(float spec, v3 in_light, v3 out_dir, v3 n) {
+  if (near_zero(sub(reflect(in_light, n), out_dir))) return spec;
+  return 0;
+}
+
+typedef struct {
+  const orc_scene* s; const pm_render_params* p; const pm_light* lights; int32_t nl;
+  const orc_map* g; const orc_map* c;
+} rctx;
+
+/* ray_colour (deviceCode.cu:25-163) */
+static v3 ray_colour(const rctx* R, v3 ro, v3 rd, prd_t* prd, cand* buf, pm_render_stats* st) {
+  int missed;
+  if (st) st->path_vertices++;
+  trace_closest(R->s, ro, rd, EPS, INFTY_F, &prd->hr, &missed, st);
+  if (missed) {
+    prd->colour = fromp(R->p->sky_colour);
+    prd->missed = 1;
+    return prd->colour;
+  }
+  prd->colour = V3(0.f, 0.f, 0.f);
+  prd->missed = 0;
+  const v3 albedo = fromp(prd->hr.mat.albedo);
+  const float diffuse_brdf = prd->hr.mat.diffuse / PI_F;
+  v3 direct = V3(0.f, 0.f, 0.f);
+  for (int l = 0; l < R->nl; l++) {
+    const pm_light* L = &R->lights[l];
+    const v3 org = prd->hr.hitpoint;
+    v3 ldir = sub(fromp(L->pos), org);
+    const float dist = norm3(ldir);
+    ldir = normalize(ldir);
+    const float ldn = dot(ldir, prd->hr.normal);
+    if (ldn < 0.f) continue;
+    int occ = any_hit(R->s, org, ldir, EPS, dist * (1.f - EPS));
+    if (st) st->rays++;
+    const float vis = occ ? 0.f : 1.f;
+    const float sb = specular_brdf(prd->hr.mat.specular, ldir, rd, prd->hr.normal);
+    const float pw = (float)L->power;
+    const float inv = 1.f / (dist * dist);
+    const float bs = diffuse_brdf + sb;
+    v3 term = V3(vis * pw * ldn * inv * bs * L->rgb.x, vis * pw * ldn * inv * bs * L->rgb.y,
+                 vis * pw * ldn * inv * bs * L->rgb.z);
+    direct = add(direct, term);
+  }
+  const v3 direct_term = mulv(albedo, direct);
+  if (st) st->caustic_queries++;
+  const v3 caustics = gather_one(R->c, prd->hr.hitpoint, diffuse_brdf, buf);
+  v3 diffuse = V3(0.f, 0.f, 0.f);
+  for (int s = 0; s < NUM_DIFFUSE_SAMPLES && diffuse_brdf > 0.f; s++) {
+    const v3 n = normalize(prd->hr.normal);
+    v3 rv, rdir;
+    do {
+      rv = random_unit_vector(&prd->rng);
+      rdir = add(n, rv);
+    } while (near_zero(rdir));
+    rdir = normalize(rdir);
+    hitrec dh;
+    memset(&dh, 0, sizeof(dh));     /* uninitialised in the reference: zeroed */
+    int dmiss;
+    trace_closest(R->s, prd->hr.hitpoint, rdir, 3 * EPS, INFTY_F, &dh, &dmiss, st);
+    if (dh.mat.diffuse > 0.f) {
+      const float sdb = dh.mat.diffuse / PI_F;
+      if (st) st->global_queries++;
+      const v3 dc = gather_one(R->g, dh.hitpoint, sdb, buf);
+      diffuse = add(diffuse, mulv(dc, fromp(dh.mat.albedo)));
+    }
+  }
+  diffuse = divf(diffuse, (float)NUM_DIFFUSE_SAMPLES);
+  diffuse = mulv(diffuse, albedo);
+  return V3(DIFFUSE_FACTOR * diffuse.x + CAUSTICS_FACTOR * caustics.x + DIRECT_LIGHT_FACTOR * direct_term.x,
+            DIFFUSE_FACTOR * diffuse.y + CAUSTICS_FACTOR * caustics.y + DIRECT_LIGHT_FACTOR * direct_term.y,
+            DIFFUSE_FACTOR * diffuse.z + CAUSTICS_FACTOR * caustics.z + DIRECT_LIGHT_FACTOR * direct_term.z);
+}
+
+/* shading.h:20-55 calculate_refracted (Random by value) */
+static v3 calculate_refracted(const pm_material* m, v3 rd, v3 n, uint32_t rng) {
+  v3 outward, refracted = V3(0.f, 0.f, 0.f);
+  float ni, R, cosine;
+  if (dot(rd, n) > 0.f) {
+    outward = neg(n);
+    ni = m->refraction_idx;
+    cosine = dot(rd, n);
+    cosine = sqrtf(1.f - m->refraction_idx * m->refraction_idx * (1.f - cosine * cosine));
+  } else {
+    outward = n;
+    ni = 1.f / m->refraction_idx;
+    cosine = -dot(rd, n);
+  }
+  if (refract_uv(rd, outward, ni, &refracted))
+    R = schlick(cosine, m->refraction_idx);
+  else
+    R = 1.f;
+  if (orc_lcg_next(&rng) < R) return reflect(rd, n);
+  return refracted;
+}
+/* shading.h:57-80 reflect_or_refract_ray (Random by value) */
+static v3 reflect_or_refract(const pm_material* m, v3 rd, v3 n, uint32_t rng, int* absorbed, float* coef) {
+  *absorbed = 0;
+  const float r = orc_lcg_next(&rng);
+  if (r < m->specular) { *coef = m->specular; return reflect(rd, n); }
+  if (r < m->specular + m->transmission) { *coef = m->transmission; return calculate_refracted(m, rd, n, rng); }
+  *coef = 0.f;
+  *absorbed = 1;
+  return V3(0.f, 0.f, 0.f);
+}
+
+static inline uint32_t make_rgba(v3 c) {
+  /* owl make_rgba: clamp(int(f*256), 0, 255) per channel, alpha 0xff; NaN -> 0 */
+  float f[3] = {c.x * 256.f, c.y * 256.f, c.z * 256.f};
+  uint32_t r = 0xffu << 24;
+  for (int i = 0; i < 3; i++) {
+    int v;
+    if (!(f[i] == f[i])) v = 0;
+    else if (f[i] >= 2147483520.f) v = 255;
+    else if (f[i] <= -2147483648.f) v = 0;
+    else v = (int)f[i];
+    if (v < 0) v = 0;
+    if (v > 255) v = 255;
+    r |= (uint32_t)v << (8 * i);
+  }
+  return r;
+}
+
+typedef struct { rctx R; int32_t row_lo, row_hi; uint32_t* rgba; float* rgb; pm_render_stats* stats;
+                 pthread_mutex_t mu; } render_ctx;
+
+/* simpleRayGen (deviceCode.cu:191-231) + tracePath (:165-189) */
+static void render_rows(void* vc, int64_t lo, int64_t hi) {
+  render_ctx* C = (render_ctx*)vc;
+  const pm_render_params* P = C->R.p;
+  cand buf[256];
+  pm_render_stats st;
+  memset(&st, 0, sizeof(st));
+  for (int64_t yy = lo; yy < hi; yy++) {
+    const int32_t py = C->row_lo + (int32_t)yy;
+    for (int32_t px = 0; px < P->width; px++) {
+      const int tile = (px / 16) + (py / 16) * ((P->width + 15) / 16);
+      if (P->tile_count > 1 && tile % P->tile_count != P->tile_rank) continue;
+      prd_t prd;
+      memset(&prd, 0, sizeof(prd));   /* zero-initialised (reference: UB) */
+      prd.rng = orc_lcg_init((uint32_t)px, (uint32_t)py);
+      v3 fc = V3(0.f, 0.f, 0.f);
+      st.pixels++;
+      for (int s = 0; s < P->samples_per_pixel; s++) {
+        const float ex = orc_lcg_next(&prd.rng);   /* vec2f(rnd(), rnd()): left to right */
+        const float ey = orc_lcg_next(&prd.rng);
+        const float su = ((float)px + ex) / (float)P->width;
+        const float sv = ((float)py + ey) / (float)P->height;
+        v3 ro = fromp(P->camera.pos);
+        v3 rd = normalize(add(add(fromp(P->camera.dir_00), smul(su, fromp(P->camera.dir_du))),
+                              smul(sv, fromp(P->camera.dir_dv))));
+        v3 colour = V3(0.f, 0.f, 0.f), att = V3(1.f, 1.f, 1.f);
+        for (int d = 0; d < P->max_depth; d++) {
+          const v3 c = ray_colour(&C->R, ro, rd, &prd, buf, &st);
+          colour = add(colour, mulv(c, att));
+          int absorbed;
+          float coef;
+          const v3 od = reflect_or_refract(&prd.hr.mat, rd, prd.hr.normal, prd.rng, &absorbed, &coef);
+          if (absorbed) break;
+          att = mulv(att, smul(coef, fromp(prd.hr.mat.albedo)));
+          ro = prd.hr.hitpoint;
+          rd = od;
+        }
+        fc = add(fc, colour);
+      }
+      fc = mulf(fc, 1.f / (float)P->samples_per_pixel);
+      const int32_t y = P->height - py;
+      if (y >= P->height) continue;    /* pixelID.y == 0 writes past the buffer: dropped */
+      const int64_t ofs = (int64_t)px + (int64_t)P->width * y;
+      if (C->rgba) C->rgba[ofs] = make_rgba(fc);
+      if (C->rgb) { C->rgb[ofs * 3] = fc.x; C->rgb[ofs * 3 + 1] = fc.y; C->rgb[ofs * 3 + 2] = fc.z; }
+    }
+  }
+  if (C->stats) {
+    pthread_mutex_lock(&C->mu);
+    C->stats->pixels += st.pixels; C->stats->path_vertices += st.path_vertices;
+    C->stats->caustic_queries += st.caustic_queries; C->stats->global_queries += st.global_queries;
+    C->stats->rays += st.rays;
+    pthread_mutex_unlock(&C->mu);
+  }
+}
+
+int orc_render(const orc_scene* s, const pm_render_params* p, const pm_light* lights, int32_t nl,
+               const orc_map* gmap, const orc_map* cmap, int32_t row_lo, int32_t row_hi,
+               int32_t nthreads, uint32_t* rgba, float* rgb, pm_render_stats* stats) {
+  if (!s || !p || !gmap || !cmap || p->width <= 0 || p->height <= 0 || p->samples_per_pixel <= 0)
+    return PM_ERR_INVALID;
+  if (row_hi <= row_lo) { row_lo = 0; row_hi = p->height; }
+  render_ctx C;
+  C.R.s = s; C.R.p = p; C.R.lights = lights; C.R.nl = nl; C.R.g = gmap; C.R.c = cmap;
+  C.row_lo = row_lo; C.row_hi = row_hi; C.rgba = rgba; C.rgb = rgb; C.stats = stats;
+  if (stats) memset(stats, 0, sizeof(*stats));
+  pthread_mutex_init(&C.mu, NULL);
+  parallel_for(row_hi - row_lo, 1, nthreads, render_rows, &C);
+  pthread_mutex_destroy(&C.mu);
+  return PM_OK;
+}

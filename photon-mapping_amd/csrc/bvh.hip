@@ -1,0 +1,288 @@
+// bvh.hip — LBVH build (Karras 2012) and ray-query kernels for gfx950.
+//
+// Replaces the OptiX GAS+IAS build of common/src/world.cpp:3-58 (loadGeometry:
+// one build input per mesh, owlGroupBuildAccel) and the RT-core traversal
+// behind every owl::traceRay / optixTrace. Pipeline: 30-bit Morton codes of
+// triangle centroids -> stable radix sort -> Karras hierarchy -> bottom-up
+// refit (agent-scope release/acquire hand-off between sibling threads) into
+// 64-B BVH2 nodes that carry both child boxes (one node fetch = both tests).
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "pm_internal.hpp"
+
+namespace pmd {
+
+__device__ __forceinline__ uint32_t expand_bits(uint32_t v) {
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+
+__global__ void k_morton(const float4* tri, int n, float3 lo, float3 inv_ext, uint32_t* codes, uint32_t* idx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 a = tri[3 * i], b = tri[3 * i + 1], c = tri[3 * i + 2];
+  const float cx = (a.x + b.x + c.x) / 3.0f, cy = (a.y + b.y + c.y) / 3.0f, cz = (a.z + b.z + c.z) / 3.0f;
+  const float fx = fminf(fmaxf((cx - lo.x) * inv_ext.x * 1024.0f, 0.0f), 1023.0f);
+  const float fy = fminf(fmaxf((cy - lo.y) * inv_ext.y * 1024.0f, 0.0f), 1023.0f);
+  const float fz = fminf(fmaxf((cz - lo.z) * inv_ext.z * 1024.0f, 0.0f), 1023.0f);
+  codes[i] = (expand_bits((uint32_t)fx) << 2) | (expand_bits((uint32_t)fy) << 1) | expand_bits((uint32_t)fz);
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void k_gather_tris(const float4* src, const uint32_t* order, int n, float4* dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t o = order[i];
+  dst[3 * i] = src[3 * o];
+  dst[3 * i + 1] = src[3 * o + 1];
+  dst[3 * i + 2] = src[3 * o + 2];
+}
+
+__device__ __forceinline__ int delta(const uint32_t* codes, int n, int i, int j) {
+  if (j < 0 || j >= n) return -1;
+  const uint32_t ci = codes[i], cj = codes[j];
+  if (ci == cj) return 32 + __clz((uint32_t)(i ^ j));
+  return __clz(ci ^ cj);
+}
+
+// Karras 2012, Fig. 4: internal node i covers [min(i,j), max(i,j)], split gamma.
+__global__ void k_hierarchy(const uint32_t* codes, int n, int4* child, int* parent_int, int* parent_leaf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n - 1) return;
+  const int d = (delta(codes, n, i, i + 1) - delta(codes, n, i, i - 1)) >= 0 ? 1 : -1;
+  const int dmin = delta(codes, n, i, i - d);
+  int lmax = 2;
+  while (delta(codes, n, i, i + lmax * d) > dmin) lmax <<= 1;
+  int l = 0;
+  for (int t = lmax >> 1; t >= 1; t >>= 1)
+    if (delta(codes, n, i, i + (l + t) * d) > dmin) l += t;
+  const int j = i + l * d;
+  const int dnode = delta(codes, n, i, j);
+  int s = 0;
+  int t = l;
+  do {
+    t = (t + 1) >> 1;
+    if (delta(codes, n, i, i + (s + t) * d) > dnode) s += t;
+  } while (t > 1);
+  const int gamma = i + s * d + min(d, 0);
+  const int lo = min(i, j), hi = max(i, j);
+  int left, right;
+  if (lo == gamma) {
+    left = ~gamma;
+    parent_leaf[gamma] = i;
+  } else {
+    left = gamma;
+    parent_int[gamma] = i;
+  }
+  if (hi == gamma + 1) {
+    right = ~(gamma + 1);
+    parent_leaf[gamma + 1] = i;
+  } else {
+    right = gamma + 1;
+    parent_int[gamma + 1] = i;
+  }
+  child[i] = make_int4(left, right, 0, 0);
+}
+
+__device__ __forceinline__ void write_child_box(float4* nodes, int node, int side, const float b[6]) {
+  // node layout: n0 = (lx0, lx1, ly0, ly1), n1 = (lz0, lz1, rx0, rx1), n2 = (ry0, ry1, rz0, rz1)
+  float* f = reinterpret_cast<float*>(&nodes[4 * node]);
+  const int base = side == 0 ? 0 : 6;
+#pragma unroll
+  for (int k = 0; k < 6; k++) f[base + k] = b[k];
+}
+
+// Bottom-up refit: each leaf walks up; the second arriving child of a node
+// unions both boxes. Hand-off per cdna_hip_programming.md Guideline 16:
+// plain stores -> release fence -> asm vmcnt(0) -> relaxed agent atomic;
+// consumer: atomic returns -> acquire fence -> loads.
+__global__ void k_refit(const float4* tri, int n, float pad, float4* nodes, const int4* child,
+                        const int* parent_int, const int* parent_leaf, unsigned* flags) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 a = tri[3 * i], b = tri[3 * i + 1], c = tri[3 * i + 2];
+  float bx[6] = {fminf(fminf(a.x, b.x), c.x) - pad, fmaxf(fmaxf(a.x, b.x), c.x) + pad,
+                 fminf(fminf(a.y, b.y), c.y) - pad, fmaxf(fmaxf(a.y, b.y), c.y) + pad,
+                 fminf(fminf(a.z, b.z), c.z) - pad, fmaxf(fmaxf(a.z, b.z), c.z) + pad};
+  int p = parent_leaf[i];
+  int me = ~i;
+  for (;;) {
+    const int4 ch = child[p];
+    write_child_box(nodes, p, ch.x == me ? 0 : 1, bx);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(&flags[p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const float* f = reinterpret_cast<const float*>(&nodes[4 * p]);
+    float u[6];
+    u[0] = fminf(__hip_atomic_load(&f[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                 __hip_atomic_load(&f[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    u[1] = fmaxf(__hip_atomic_load(&f[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                 __hip_atomic_load(&f[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    u[2] = fminf(__hip_atomic_load(&f[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                 __hip_atomic_load(&f[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    u[3] = fmaxf(__hip_atomic_load(&f[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                 __hip_atomic_load(&f[9], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    u[4] = fminf(__hip_atomic_load(&f[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                 __hip_atomic_load(&f[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    u[5] = fmaxf(__hip_atomic_load(&f[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                 __hip_atomic_load(&f[11], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+    for (int k = 0; k < 6; k++) bx[k] = u[k];
+    if (p == 0) return;
+    me = p;
+    p = parent_int[p];
+  }
+}
+
+__global__ void k_pack_children(float4* nodes, const int4* child, int nn) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nn) return;
+  nodes[4 * i + 3] = *reinterpret_cast<const float4*>(&child[i]);
+}
+
+__global__ void k_leaf_depth(const int* parent_int, const int* parent_leaf, int n, int* maxdepth) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int d = 1;
+  int p = parent_leaf[i];
+  while (p != 0 && d < (1 << 20)) {
+    p = parent_int[p];
+    d++;
+  }
+  atomicMax(maxdepth, d);
+}
+
+hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s) {
+  const int n = sc->ntri;
+  if (n == 0) {
+    sc->nnodes = 0;
+    sc->depth = 0;
+    return hipSuccess;
+  }
+  float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  float clo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, chi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = 0; i < n; i++) {
+    const float4 v[3] = {th[3 * i], th[3 * i + 1], th[3 * i + 2]};
+    float c[3] = {0, 0, 0};
+    for (int k = 0; k < 3; k++) {
+      const float vx = v[k].x, vy = v[k].y, vz = v[k].z;
+      lo[0] = std::min(lo[0], vx); hi[0] = std::max(hi[0], vx);
+      lo[1] = std::min(lo[1], vy); hi[1] = std::max(hi[1], vy);
+      lo[2] = std::min(lo[2], vz); hi[2] = std::max(hi[2], vz);
+      c[0] += vx; c[1] += vy; c[2] += vz;
+    }
+    for (int k = 0; k < 3; k++) {
+      clo[k] = std::min(clo[k], c[k] / 3.0f);
+      chi[k] = std::max(chi[k], c[k] / 3.0f);
+    }
+  }
+  float ext = 0.f;
+  for (int k = 0; k < 3; k++) ext = std::max(ext, hi[k] - lo[k]);
+  const float pad = ext * 1e-5f + 1e-20f;
+  sc->bounds = {{lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}};
+
+  DevBuf<float4> tri_orig((size_t)3 * n);
+  sc->tri.alloc((size_t)3 * n);
+  const int nn = std::max(1, n - 1);
+  sc->nodes.alloc((size_t)4 * nn);
+  if (!tri_orig.p || !sc->tri.p || !sc->nodes.p) return hipErrorOutOfMemory;
+  PM_HIP_TRY(hipMemcpyAsync(tri_orig.p, th.data(), sizeof(float4) * 3 * n, hipMemcpyHostToDevice, s));
+  sc->nnodes = nn;
+  if (n == 1) {
+    PM_HIP_TRY(hipMemcpyAsync(sc->tri.p, tri_orig.p, sizeof(float4) * 3, hipMemcpyDeviceToDevice, s));
+    const float4 a = th[0], b = th[1], c = th[2];
+    float bx[6] = {std::min({a.x, b.x, c.x}) - pad, std::max({a.x, b.x, c.x}) + pad,
+                   std::min({a.y, b.y, c.y}) - pad, std::max({a.y, b.y, c.y}) + pad,
+                   std::min({a.z, b.z, c.z}) - pad, std::max({a.z, b.z, c.z}) + pad};
+    float node[16];
+    for (int k = 0; k < 6; k++) node[k] = bx[k], node[6 + k] = bx[k];
+    const int ch[4] = {~0, ~0, 0, 0};
+    std::memcpy(&node[12], ch, 16);
+    PM_HIP_TRY(hipMemcpyAsync(sc->nodes.p, node, 64, hipMemcpyHostToDevice, s));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    sc->depth = 1;
+    return hipSuccess;
+  }
+  DevBuf<uint32_t> codes(n), order(n);
+  DevBuf<int4> child(nn);
+  DevBuf<int> pint(nn), pleaf(n), depth(1);
+  DevBuf<unsigned> flags(nn);
+  if (!codes.p || !order.p || !child.p || !pint.p || !pleaf.p || !flags.p || !depth.p) return hipErrorOutOfMemory;
+  float3 clo3 = make_float3(clo[0], clo[1], clo[2]);
+  float3 inv = make_float3(chi[0] > clo[0] ? 1.0f / (chi[0] - clo[0]) : 0.f,
+                           chi[1] > clo[1] ? 1.0f / (chi[1] - clo[1]) : 0.f,
+                           chi[2] > clo[2] ? 1.0f / (chi[2] - clo[2]) : 0.f);
+  k_morton<<<grid_for(n, 256), 256, 0, s>>>(tri_orig.p, n, clo3, inv, codes.p, order.p);
+  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(radix_sort_pairs(codes.p, order.p, n, 30, s));
+  k_gather_tris<<<grid_for(n, 256), 256, 0, s>>>(tri_orig.p, order.p, n, sc->tri.p);
+  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(hipMemsetAsync(pint.p, 0, sizeof(int) * nn, s));
+  k_hierarchy<<<grid_for(n - 1, 256), 256, 0, s>>>(codes.p, n, child.p, pint.p, pleaf.p);
+  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(hipMemsetAsync(flags.p, 0, sizeof(unsigned) * nn, s));
+  k_refit<<<grid_for(n, 256), 256, 0, s>>>(sc->tri.p, n, pad, sc->nodes.p, child.p, pint.p, pleaf.p, flags.p);
+  PM_HIP_TRY(hipGetLastError());
+  k_pack_children<<<grid_for(nn, 256), 256, 0, s>>>(sc->nodes.p, child.p, nn);
+  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(hipMemsetAsync(depth.p, 0, sizeof(int), s));
+  k_leaf_depth<<<grid_for(n, 256), 256, 0, s>>>(pint.p, pleaf.p, n, depth.p);
+  PM_HIP_TRY(hipGetLastError());
+  int dh = 0;
+  PM_HIP_TRY(hipMemcpyAsync(&dh, depth.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  PM_HIP_TRY(hipStreamSynchronize(s));
+  sc->depth = dh;
+  return hipSuccess;
+}
+
+// ---------------------------------------------------------------- queries
+constexpr int kQBlock = 128;
+
+template <bool ANY>
+__global__ __launch_bounds__(kQBlock) void k_query(DevScene S, const pm_ray* rays, int64_t n, pm_hit* hits,
+                                                   int32_t* occ, int* overflow) {
+  __shared__ int stack[kStackDepth * kQBlock];
+  const int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x;
+  if (i >= n) return;
+  const pm_ray R = rays[i];
+  Ray r;
+  ray_prep(r, mk(R.origin), mk(R.direction));
+  HitInfo h = traverse<ANY>(S, r, R.tmin, R.tmax, stack + threadIdx.x, kQBlock, overflow);
+  if (ANY) {
+    occ[i] = h.slot >= 0 ? 1 : 0;
+  } else {
+    pm_hit o;
+    if (h.slot < 0) {
+      o.t = INFINITY;
+      o.mesh = o.prim = o.tri = -1;
+    } else {
+      const float4 a = S.tri[3 * h.slot], b = S.tri[3 * h.slot + 1];
+      o.t = h.t;
+      o.mesh = __float_as_int(a.w);
+      o.prim = __float_as_int(b.w);
+      o.tri = h.gid;
+    }
+    hits[i] = o;
+  }
+}
+
+hipError_t launch_query(pm_scene* sc, const pm_ray* rays, int64_t n, pm_hit* hits, int32_t* occ, bool any,
+                        hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (any)
+    k_query<true><<<grid_for(n, kQBlock), kQBlock, 0, s>>>(sc->view(), rays, n, hits, occ, sc->overflow.p);
+  else
+    k_query<false><<<grid_for(n, kQBlock), kQBlock, 0, s>>>(sc->view(), rays, n, hits, occ, sc->overflow.p);
+  return hipGetLastError();
+}
+
+}  // namespace pmd

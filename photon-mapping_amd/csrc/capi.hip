@@ -1,0 +1,483 @@
+// capi.hip — the extern "C" boundary of libpm_hip.so (declared in include/pm.h).
+//
+// Mirrors the reference's host-side entry points for the hot path:
+//   pm_scene_create      <- loadGeometry (common/src/world.cpp:3-58)
+//   pm_trace_photons     <- runNormal / runCaustics / runPointLightRayGen
+//                           (photon-mapping/src/hostCode.cu:72-138)
+//   pm_photon_map_create <- loadPhotons (ray-tracer/src/hostCode.cu:54-99)
+//   pm_kdtree_build      <- cukd::buildTree (ray-tracer/src/hostCode.cu:94-95)
+//   pm_knn / pm_gather   <- KNearestPhotons / gatherPhotons (ray-tracer/cuda/shading.h)
+//   pm_render            <- owlRayGenLaunch2D(simpleRayGen) (ray-tracer/src/hostCode.cu:231-237)
+// Every compute entry point runs on the GPU; without a device it returns
+// PM_ERR_NO_DEVICE (there is no CPU fallback).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "pm_internal.hpp"
+
+namespace pmd {
+
+hipError_t launch_query(pm_scene* sc, const pm_ray* rays, int64_t n, pm_hit* hits, int32_t* occ, bool any,
+                        hipStream_t s);
+struct LightDev {
+  float4 pos;
+  float4 rgb;
+};
+hipError_t launch_trace_chunk(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl, int64_t g_lo,
+                              int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt, hipStream_t s);
+hipError_t launch_compact(const pm_photon* slots, const uint32_t* cnt, const uint32_t* off, int64_t np,
+                          pm_photon* out, hipStream_t s);
+hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
+                                     float pb, float4* elems, float4* payload, hipStream_t s);
+hipError_t kd_build_records(pm_kd_photon* d, int64_t n, pm_box* bounds, hipStream_t s);
+hipError_t launch_map_export(const pm_photon_map* m, pm_kd_photon* out, hipStream_t s);
+hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int k, float radius, int32_t* ids,
+                      float* d2, float* maxd2, hipStream_t s);
+hipError_t launch_gather_api(const pm_photon_map* m, const pm_float3* pts, const float* brdf, int64_t nq,
+                             pm_float3* out, hipStream_t s);
+hipError_t render_impl(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int nl,
+                       const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba, float* rgb,
+                       pm_render_stats* stats, hipStream_t s);
+
+namespace {
+std::mutex g_phase_mu;
+double g_phase_us[PH_COUNT] = {0};
+pm_render_stats g_render_stats{};
+}  // namespace
+
+void record_phase_us(int phase, double us) {
+  std::lock_guard<std::mutex> lk(g_phase_mu);
+  if (phase >= 0 && phase < PH_COUNT) g_phase_us[phase] += us;
+}
+static void reset_phase(int phase) {
+  std::lock_guard<std::mutex> lk(g_phase_mu);
+  if (phase >= 0 && phase < PH_COUNT) g_phase_us[phase] = 0;
+}
+
+PhaseTimer::PhaseTimer(int ph, hipStream_t st) : s(st), phase(ph) {
+  if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+    a = b = nullptr;
+    return;
+  }
+  (void)hipEventRecord(a, s);
+}
+PhaseTimer::~PhaseTimer() {
+  if (!a) return;
+  (void)hipEventRecord(b, s);
+  if (hipEventSynchronize(b) == hipSuccess) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) == hipSuccess) record_phase_us(phase, (double)ms * 1000.0);
+  }
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+}
+
+}  // namespace pmd
+
+using namespace pmd;
+
+namespace {
+
+int map_err(hipError_t e) {
+  if (e == hipSuccess) return PM_OK;
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return PM_ERR_OOM;
+  if (e == hipErrorInvalidValue) return PM_ERR_INVALID;
+  if (e == hipErrorNoDevice) return PM_ERR_NO_DEVICE;
+  std::fprintf(stderr, "pm: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
+  return PM_ERR_HIP;
+}
+
+int require_device() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return PM_ERR_NO_DEVICE;
+  }
+  return PM_OK;
+}
+
+int check_overflow(pm_scene* sc, hipStream_t s) {
+  int ov = 0;
+  if (hipMemcpyAsync(&ov, sc->overflow.p, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return PM_ERR_HIP;
+  return ov ? PM_ERR_OVERFLOW : PM_OK;
+}
+
+#define PM_TRY_ST(expr)             \
+  do {                              \
+    int _st = map_err(expr);        \
+    if (_st != PM_OK) return _st;   \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int pm_abi_version(void) { return PM_ABI_VERSION; }
+
+const char* pm_status_string(int st) {
+  switch (st) {
+    case PM_OK: return "ok";
+    case PM_ERR_INVALID: return "invalid argument";
+    case PM_ERR_HIP: return "HIP runtime error";
+    case PM_ERR_OOM: return "device out of memory";
+    case PM_ERR_NO_DEVICE: return "no HIP device";
+    case PM_ERR_IO: return "I/O error";
+    case PM_ERR_CAPACITY: return "output capacity too small";
+    case PM_ERR_OVERFLOW: return "traversal stack overflow";
+    default: return "unknown status";
+  }
+}
+
+int pm_device_count(int32_t* count) {
+  if (!count) return PM_ERR_INVALID;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  *count = n;
+  return PM_OK;
+}
+
+int pm_last_phase_us(int32_t phase, double* us) {
+  if (!us || phase < 0 || phase >= PH_COUNT) return PM_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(g_phase_mu);
+  *us = g_phase_us[phase];
+  return PM_OK;
+}
+
+// ------------------------------------------------------------------ scene
+int pm_scene_create(const pm_mesh* meshes, int32_t num_meshes, pm_scene** out) {
+  if (!out || num_meshes < 0 || (num_meshes > 0 && !meshes)) return PM_ERR_INVALID;
+  *out = nullptr;
+  int st = require_device();
+  if (st != PM_OK) return st;
+  std::vector<float4> th;
+  std::vector<float4> mh;
+  int64_t gid = 0;
+  for (int m = 0; m < num_meshes; m++) {
+    const pm_mesh& M = meshes[m];
+    if (M.num_triangles < 0 || M.num_vertices < 0 || (M.num_triangles > 0 && (!M.indices || !M.vertices)))
+      return PM_ERR_INVALID;
+    for (int j = 0; j < M.num_triangles; j++, gid++) {
+      const pm_int3 ix = M.indices[j];
+      const int32_t id3[3] = {ix.x, ix.y, ix.z};
+      for (int k = 0; k < 3; k++)
+        if (id3[k] < 0 || id3[k] >= M.num_vertices) return PM_ERR_INVALID;
+      const pm_float3 A = M.vertices[ix.x], B = M.vertices[ix.y], C = M.vertices[ix.z];
+      float wa, wb, wc;
+      const int32_t im = m, ip = j, ig = (int32_t)gid;
+      std::memcpy(&wa, &im, 4);
+      std::memcpy(&wb, &ip, 4);
+      std::memcpy(&wc, &ig, 4);
+      th.push_back(make_float4(A.x, A.y, A.z, wa));
+      th.push_back(make_float4(B.x, B.y, B.z, wb));
+      th.push_back(make_float4(C.x, C.y, C.z, wc));
+    }
+    const pm_material& mt = M.material;
+    mh.push_back(make_float4(mt.albedo.x, mt.albedo.y, mt.albedo.z, mt.diffuse));
+    mh.push_back(make_float4(mt.specular, mt.transmission, mt.refraction_idx, 0.f));
+  }
+  if (gid >= (1ll << 31)) return PM_ERR_INVALID;
+  pm_scene* sc = new pm_scene;
+  sc->ntri = (int32_t)gid;
+  sc->nmesh = num_meshes;
+  for (int m = 0; m < num_meshes; m++) sc->host_mat.push_back(meshes[m].material);
+  hipStream_t s = nullptr;
+  sc->mat.alloc(std::max<size_t>(mh.size(), 2));
+  sc->overflow.alloc(1);
+  if (!sc->mat.p || !sc->overflow.p) {
+    delete sc;
+    return PM_ERR_OOM;
+  }
+  hipError_t e = hipSuccess;
+  if (!mh.empty()) e = hipMemcpyAsync(sc->mat.p, mh.data(), sizeof(float4) * mh.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemsetAsync(sc->overflow.p, 0, sizeof(int32_t), s);
+  reset_phase(PH_BVH);
+  if (e == hipSuccess) {
+    PhaseTimer tm(PH_BVH, s);
+    e = build_lbvh(sc, th, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    delete sc;
+    return map_err(e);
+  }
+  *out = sc;
+  return PM_OK;
+}
+
+int pm_scene_stats_get(const pm_scene* sc, pm_scene_stats* o) {
+  if (!sc || !o) return PM_ERR_INVALID;
+  o->num_triangles = sc->ntri;
+  o->num_nodes = sc->nnodes;
+  o->num_meshes = sc->nmesh;
+  o->max_depth = sc->depth;
+  o->bounds = sc->bounds;
+  return PM_OK;
+}
+
+int pm_scene_destroy(pm_scene* sc) {
+  delete sc;
+  return PM_OK;
+}
+
+int pm_scene_intersect(pm_scene* sc, const pm_ray* rays, int64_t n, pm_hit* hits, void* stream) {
+  if (!sc || n < 0 || (n > 0 && (!rays || !hits))) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  PM_TRY_ST(launch_query(sc, rays, n, hits, nullptr, false, s));
+  return check_overflow(sc, s);
+}
+
+int pm_scene_occluded(pm_scene* sc, const pm_ray* rays, int64_t n, int32_t* occ, void* stream) {
+  if (!sc || n < 0 || (n > 0 && (!rays || !occ))) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  PM_TRY_ST(launch_query(sc, rays, n, nullptr, occ, true, s));
+  return check_overflow(sc, s);
+}
+
+// ------------------------------------------------------------------ stage 1
+int pm_photons_per_light(const pm_light* lights, int32_t nl, int64_t casted, int64_t* counts) {
+  if (nl < 0 || (nl > 0 && (!lights || !counts))) return PM_ERR_INVALID;
+  // computePhotonsPerWatt (hostCode.cu:102-110): int photonsPerWatt = int / double
+  double total = 0;
+  for (int i = 0; i < nl; i++) total += lights[i].power;
+  if (!(total > 0.0)) {
+    for (int i = 0; i < nl; i++) counts[i] = 0;
+    return PM_OK;
+  }
+  const int ppw = (int)((double)(int)casted / total);
+  for (int i = 0; i < nl; i++) counts[i] = (int64_t)(int)(lights[i].power * ppw);   // hostCode.cu:86
+  return PM_OK;
+}
+
+static int shard_range(const pm_light* lights, int32_t nl, const pm_trace_params* p, std::vector<int64_t>& loff,
+                       int64_t& lo, int64_t& hi) {
+  if (!p || p->shard_count < 1 || p->shard_rank < 0 || p->shard_rank >= p->shard_count || p->max_depth < 0 ||
+      p->max_depth > 255 || p->casted_photons < 0)
+    return PM_ERR_INVALID;
+  std::vector<int64_t> cnt(nl > 0 ? nl : 1, 0);
+  int st = pm_photons_per_light(lights, nl, p->casted_photons, cnt.data());
+  if (st != PM_OK) return st;
+  loff.assign(nl + 1, 0);
+  for (int i = 0; i < nl; i++) loff[i + 1] = loff[i] + std::max<int64_t>(cnt[i], 0);
+  const int64_t tot = loff[nl];
+  lo = tot * p->shard_rank / p->shard_count;
+  hi = tot * (p->shard_rank + 1) / p->shard_count;
+  return PM_OK;
+}
+
+int pm_trace_capacity(const pm_light* lights, int32_t nl, const pm_trace_params* p, int64_t* capacity) {
+  if (!capacity) return PM_ERR_INVALID;
+  std::vector<int64_t> loff;
+  int64_t lo, hi;
+  int st = shard_range(lights, nl, p, loff, lo, hi);
+  if (st != PM_OK) return st;
+  const int per = p->caustics_mode ? 1 : std::max(p->max_depth - 1, 0);
+  *capacity = (hi - lo) * per;
+  return PM_OK;
+}
+
+int pm_trace_photons(pm_scene* sc, const pm_light* lights, int32_t nl, const pm_trace_params* p, pm_photon* d_out,
+                     int64_t capacity, int64_t* count, void* stream) {
+  if (!sc || !count || capacity < 0) return PM_ERR_INVALID;
+  *count = 0;
+  std::vector<int64_t> loff;
+  int64_t lo, hi;
+  int st = shard_range(lights, nl, p, loff, lo, hi);
+  if (st != PM_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  reset_phase(PH_TRACE);
+  reset_phase(PH_COMPACT);
+  const int maxd = p->max_depth;
+  const int per = p->caustics_mode ? 1 : std::max(maxd - 1, 0);
+  const int64_t np_total = hi - lo;
+  if (np_total <= 0 || per == 0 || nl == 0) return PM_OK;
+  std::vector<LightDev> lh(nl);
+  for (int i = 0; i < nl; i++) {
+    lh[i].pos = make_float4(lights[i].pos.x, lights[i].pos.y, lights[i].pos.z, 0.f);
+    lh[i].rgb = make_float4(lights[i].rgb.x, lights[i].rgb.y, lights[i].rgb.z, 0.f);
+  }
+  DevBuf<LightDev> dl(nl);
+  DevBuf<int64_t> dloff(nl + 1);
+  if (!dl.p || !dloff.p) return PM_ERR_OOM;
+  PM_TRY_ST(hipMemcpyAsync(dl.p, lh.data(), sizeof(LightDev) * nl, hipMemcpyHostToDevice, s));
+  PM_TRY_ST(hipMemcpyAsync(dloff.p, loff.data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
+  // chunk so that the deposit slots stay below ~3 GB
+  int64_t chunk = std::min<int64_t>(np_total, std::max<int64_t>(1 << 16, (int64_t)3e9 / (40ll * per)));
+  chunk = std::min<int64_t>(chunk, 1ll << 26);
+  DevBuf<pm_photon> slots((size_t)chunk * per);
+  DevBuf<uint32_t> cnt(chunk), off(chunk), tot(1);
+  if (!slots.p || !cnt.p || !off.p || !tot.p) return PM_ERR_OOM;
+  int64_t written = 0;
+  bool over = false;
+  for (int64_t g0 = lo; g0 < hi; g0 += chunk) {
+    const int64_t np = std::min(chunk, hi - g0);
+    {
+      PhaseTimer tm(PH_TRACE, s);
+      PM_TRY_ST(launch_trace_chunk(sc, dl.p, dloff.p, nl, g0, np, maxd, p->caustics_mode ? 1 : 0, slots.p, cnt.p,
+                                   s));
+    }
+    uint32_t t = 0;
+    {
+      PhaseTimer tm(PH_COMPACT, s);
+      PM_TRY_ST(exclusive_scan_u32(cnt.p, off.p, np, tot.p, s));
+      PM_TRY_ST(hipMemcpyAsync(&t, tot.p, 4, hipMemcpyDeviceToHost, s));
+      PM_TRY_ST(hipStreamSynchronize(s));
+      if (!over && written + (int64_t)t <= capacity && d_out) {
+        PM_TRY_ST(launch_compact(slots.p, cnt.p, off.p, np, d_out + written, s));
+      } else {
+        over = true;
+      }
+    }
+    written += t;
+  }
+  PM_TRY_ST(hipStreamSynchronize(s));
+  *count = written;
+  st = check_overflow(sc, s);
+  if (st != PM_OK) return st;
+  return over ? PM_ERR_CAPACITY : PM_OK;
+}
+
+// ------------------------------------------------------------------ stage 2
+int pm_kdtree_build(pm_kd_photon* d, int64_t n, pm_box* bounds, void* stream) {
+  if (n < 0 || (n > 0 && !d)) return PM_ERR_INVALID;
+  int st = require_device();
+  if (st != PM_OK) return st;
+  if (n >= (1ll << 30)) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  reset_phase(PH_KDBUILD);
+  PhaseTimer tm(PH_KDBUILD, s);
+  return map_err(kd_build_records(d, n, bounds, s));
+}
+
+int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_photon* b, int64_t nb, float pb,
+                         pm_photon_map** out, void* stream) {
+  if (!out || na < 0 || nb < 0 || (na > 0 && !a) || (nb > 0 && !b)) return PM_ERR_INVALID;
+  *out = nullptr;
+  int st = require_device();
+  if (st != PM_OK) return st;
+  const int64_t n = na + nb;
+  if (n >= (1ll << 30)) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  pm_photon_map* m = new pm_photon_map;
+  m->n = n;
+  if (n > 0) {
+    m->nodes.alloc(n);
+    m->payload.alloc(n);
+    DevBuf<float4> elems(n);
+    if (!m->nodes.p || !m->payload.p || !elems.p) {
+      delete m;
+      return PM_ERR_OOM;
+    }
+    reset_phase(PH_KDBUILD);
+    hipError_t e;
+    {
+      PhaseTimer tm(PH_KDBUILD, s);
+      e = launch_elems_from_photons(a, na, b, nb, pa, pb, elems.p, m->payload.p, s);
+      if (e == hipSuccess) e = kd_build(elems.p, n, m->nodes.p, s);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+      delete m;
+      return map_err(e);
+    }
+  }
+  *out = m;
+  return PM_OK;
+}
+
+int pm_photon_map_size(const pm_photon_map* m, int64_t* n) {
+  if (!m || !n) return PM_ERR_INVALID;
+  *n = m->n;
+  return PM_OK;
+}
+
+int pm_photon_map_export(const pm_photon_map* m, pm_kd_photon* d_out, void* stream) {
+  if (!m || (m->n > 0 && !d_out)) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  PM_TRY_ST(launch_map_export(m, d_out, s));
+  return map_err(hipStreamSynchronize(s));
+}
+
+int pm_photon_map_destroy(pm_photon_map* m) {
+  delete m;
+  return PM_OK;
+}
+
+int pm_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int32_t k, float max_radius, int32_t* ids,
+           float* d2, float* maxd2, void* stream) {
+  if (!m || nq < 0 || k < 1 || k > 128 || (nq > 0 && (!q || !ids)) || !(max_radius >= 0.f)) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  PM_TRY_ST(launch_knn(m, q, nq, k, max_radius, ids, d2, maxd2, s));
+  return map_err(hipStreamSynchronize(s));
+}
+
+int pm_gather(const pm_photon_map* m, const pm_float3* pts, const float* brdf, int64_t nq, pm_float3* out,
+              void* stream) {
+  if (!m || nq < 0 || (nq > 0 && (!pts || !brdf || !out))) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  reset_phase(PH_GATHER);
+  PhaseTimer tm(PH_GATHER, s);
+  return map_err(launch_gather_api(m, pts, brdf, nq, out, s));
+}
+
+int pm_camera_setup(pm_float3 from, pm_float3 at, pm_float3 up, float fovy, int32_t w, int32_t h, pm_camera* o) {
+  if (!o || w <= 0 || h <= 0) return PM_ERR_INVALID;
+  // setupCamera (ray-tracer/src/hostCode.cu:100-108), owl vec3f arithmetic
+  struct V {
+    float x, y, z;
+  };
+  auto sub = [](V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; };
+  auto add = [](V a, V b) { return V{a.x + b.x, a.y + b.y, a.z + b.z}; };
+  auto smul = [](float s, V a) { return V{s * a.x, s * a.y, s * a.z}; };
+  auto dot = [](V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; };
+  auto cross = [](V a, V b) { return V{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; };
+  auto norm = [&](V v) {
+    const float r = 1.0f / std::sqrt(dot(v, v));
+    return V{v.x * r, v.y * r, v.z * r};
+  };
+  const float aspect = (float)w / (float)h;
+  const float cf = std::cos(fovy);
+  const V F{from.x, from.y, from.z}, A{at.x, at.y, at.z}, U{up.x, up.y, up.z};
+  V d00 = norm(sub(A, F));
+  const V du = smul(cf * aspect, norm(cross(d00, U)));
+  const V dv = smul(cf, norm(cross(du, d00)));
+  d00 = sub(d00, smul(0.5f, add(du, dv)));
+  o->pos = from;
+  o->dir_00 = {d00.x, d00.y, d00.z};
+  o->dir_du = {du.x, du.y, du.z};
+  o->dir_dv = {dv.x, dv.y, dv.z};
+  return PM_OK;
+}
+
+int pm_render(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int32_t nl,
+              const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba, float* rgb, void* stream) {
+  if (!sc || !P || !gmap || !cmap || !rgba || nl < 0 || (nl > 0 && !lights) || P->width <= 0 || P->height <= 0 ||
+      P->samples_per_pixel <= 0 || P->max_depth < 0 || (P->tile_count > 1 && (P->tile_rank < 0 ||
+                                                                             P->tile_rank >= P->tile_count)))
+    return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  reset_phase(PH_PATHS);
+  reset_phase(PH_GATHER);
+  reset_phase(PH_RESOLVE);
+  pm_render_stats stats{};
+  PM_TRY_ST(render_impl(sc, P, lights, nl, gmap, cmap, rgba, rgb, &stats, s));
+  PM_TRY_ST(hipStreamSynchronize(s));
+  g_render_stats = stats;
+  return check_overflow(sc, s);
+}
+
+int pm_render_stats_get(pm_render_stats* o) {
+  if (!o) return PM_ERR_INVALID;
+  *o = g_render_stats;
+  return PM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,342 @@
+// pm_device.hpp — device-side arithmetic for the photon-mapping hot path (gfx950).
+//
+// Every function here implements the arithmetic spec of DESIGN.md §2 so that
+// the HIP kernels and the CPU oracle (oracle/pm_oracle.c, an independent C
+// restatement) compute bit-identical floats. Compiled with
+// -ffp-contract=off (no FMA contraction) and correctly rounded f32 div/sqrt.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pm.h"
+
+namespace pmd {
+
+constexpr float kEPS = 1e-3f;                       // common/cuda/helpers.h:8
+constexpr float kPI = (float)3.141592653;            // helpers.h:9
+constexpr float kINFTY = 1e10f;                      // helpers.h:7
+constexpr float kPhotonTmax = 1e30f;                 // owl::Ray default tmax
+constexpr int kKNearest = 50;                        // ray-tracer/cuda/shading.h:7
+constexpr float kKMaxDistance = 100.0f;              // shading.h:8
+constexpr float kConeFilterC = 1.1f;                 // shading.h:9
+constexpr int kNumDiffuseSamples = 20;               // ray-tracer/cuda/deviceCode.cu:15
+constexpr float kDirectLightFactor = 0.8f;           // deviceCode.cu:10
+constexpr float kCausticsFactor = 0.08f;             // deviceCode.cu:11
+constexpr float kDiffuseFactor = 0.2f;               // deviceCode.cu:12
+
+enum { EV_MISS = 0, EV_ABSORBED = 1, EV_DIFFUSE = 2, EV_SPECULAR = 4, EV_REFRACT = 8 };
+
+struct v3 {
+  float x, y, z;
+};
+__host__ __device__ __forceinline__ v3 mk(float x, float y, float z) { return {x, y, z}; }
+__host__ __device__ __forceinline__ v3 mk(pm_float3 p) { return {p.x, p.y, p.z}; }
+__device__ __forceinline__ v3 add(v3 a, v3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ v3 sub(v3 a, v3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ v3 mulf(v3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ v3 smul(float s, v3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ v3 mulv(v3 a, v3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ v3 divf(v3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ v3 neg(v3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ v3 cross(v3 a, v3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+// owl normalize(v) = v * rsqrt(dot(v,v)); spec: rsqrt := 1/sqrtf (IEEE)
+__device__ __forceinline__ v3 normalize(v3 v) { return mulf(v, 1.0f / sqrtf(dot(v, v))); }
+__device__ __forceinline__ float norm3(v3 v) { return sqrtf(dot(v, v)); }
+__device__ __forceinline__ bool near_zero(v3 v) { return v.x < kEPS && v.y < kEPS && v.z < kEPS; }
+__device__ __forceinline__ float comp(v3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+// owl::LCG<16>
+__device__ __forceinline__ uint32_t lcg_init(uint32_t val0, uint32_t val1) {
+  uint32_t v0 = val0, v1 = val1, s0 = 0;
+#pragma unroll
+  for (int n = 0; n < 16; n++) {
+    s0 += 0x9e3779b9u;
+    v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + s0) ^ ((v1 >> 5) + 0xc8013ea4u);
+    v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + s0) ^ ((v0 >> 5) + 0x7e95761eu);
+  }
+  return v0;
+}
+__device__ __forceinline__ float lcg_next(uint32_t& st) {
+  st = 1664525u * st + 1013904223u;
+  return (float)(st & 0x00FFFFFFu) / (float)0x01000000;
+}
+
+// Deterministic acos / sincos
+__device__ __forceinline__ float acos_spec(float x) {
+  float ax = fabsf(x);
+  float p = -0.0012624911f;
+  p = p * ax + 0.0066700901f;
+  p = p * ax + -0.0170881256f;
+  p = p * ax + 0.0308918810f;
+  p = p * ax + -0.0501743046f;
+  p = p * ax + 0.0889789874f;
+  p = p * ax + -0.2145988016f;
+  p = p * ax + 1.5707963050f;
+  float r = sqrtf(1.0f - ax) * p;
+  return x < 0.0f ? 3.14159274f - r : r;
+}
+__device__ __forceinline__ void sincos_spec(float x, float& s, float& c) {
+  float q = rintf(x * 0.636619772f);
+  int k = (int)q;
+  float r = x - q * 1.5703125f;
+  r = r - q * 4.837512969970703125e-4f;
+  r = r - q * 7.549789954891882e-8f;
+  float r2 = r * r;
+  float sp = -1.9515295891e-4f;
+  sp = sp * r2 + 8.3321608736e-3f;
+  sp = sp * r2 + -1.6666654611e-1f;
+  sp = sp * r2;
+  sp = sp * r;
+  sp = sp + r;
+  float cp = 2.443315711809948e-5f;
+  cp = cp * r2 + -1.388731625493765e-3f;
+  cp = cp * r2 + 4.166664568298827e-2f;
+  cp = cp * (r2 * r2);
+  cp = (1.0f - 0.5f * r2) + cp;
+  switch (k & 3) {
+    case 0: s = sp; c = cp; break;
+    case 1: s = cp; c = -sp; break;
+    case 2: s = -sp; c = -cp; break;
+    default: s = -cp; c = sp; break;
+  }
+}
+
+// helpers.h:27-34
+__device__ __forceinline__ v3 random_point_in_unit_sphere(uint32_t& st) {
+  const float u = lcg_next(st);
+  const float v = lcg_next(st);
+  const float theta = 2.f * kPI * u;
+  const float phi = acos_spec(2.f * v - 1.f);
+  float sp, cp, sth, cth;
+  sincos_spec(phi, sp, cp);
+  sincos_spec(theta, sth, cth);
+  return {sp * cth, sp * sth, cp};
+}
+// helpers.h:36-43
+__device__ __forceinline__ v3 random_unit_vector(uint32_t& st) {
+  v3 v;
+  do {
+    v.x = 2.f * lcg_next(st) - 1.f;
+    v.y = 2.f * lcg_next(st) - 1.f;
+    v.z = 2.f * lcg_next(st) - 1.f;
+  } while (dot(v, v) >= 1.f);
+  return normalize(v);
+}
+// helpers.h:45-51
+__device__ __forceinline__ v3 cosine_sample_hemisphere(v3 n, uint32_t& st) {
+  return normalize(add(n, mulf(random_point_in_unit_sphere(st), (1 - kEPS))));
+}
+__device__ __forceinline__ v3 reflect(v3 i, v3 n) { return sub(i, mulf(n, 2.f * dot(i, n))); }
+// helpers.h:57-74
+__device__ __forceinline__ v3 refract_ior(v3 in, v3 n, float ior) {
+  float ct = -dot(in, n);
+  float mu;
+  if (ct > 0.f) {
+    mu = 1.f / ior;
+  } else {
+    mu = ior;
+    ct = -ct;
+  }
+  const float cphi = 1.f - mu * mu * (1.f - ct * ct);
+  if (cphi >= 0) return add(smul(mu, in), smul(mu * ct - sqrtf(cphi), n));
+  return reflect(in, n);
+}
+// helpers.h:91-106
+__device__ __forceinline__ bool refract_uv(v3 v, v3 n, float ni, v3& refracted) {
+  const v3 uv = normalize(v);
+  const float dt = dot(uv, n);
+  const float disc = 1.0f - ni * ni * (1 - dt * dt);
+  if (disc > 0.f) {
+    refracted = sub(smul(ni, sub(uv, mulf(n, dt))), mulf(n, sqrtf(disc)));
+    return true;
+  }
+  return false;
+}
+// helpers.h:108-112 (double; pow(x,5) := ((x*x)*(x*x))*x)
+__device__ __forceinline__ float schlick(float cosv, float ior) {
+  float r0 = (float)((1. - (double)ior) / (1. + (double)ior));
+  r0 = r0 * r0;
+  double x = 1. - (double)cosv;
+  double x2 = x * x;
+  double p5 = (x2 * x2) * x;
+  return (float)((double)r0 + (1. - (double)r0) * p5);
+}
+
+// ---------------------------------------------------------------- scene
+// Triangle record (48 B, 3 x float4): A.xyz|mesh, B.xyz|prim, C.xyz|global tri id.
+// BVH2 node (64 B): left box, right box, child ids (>=0 internal, <0 leaf ~slot).
+struct DevScene {
+  const float4* tri;       // [3*T] in leaf (Morton) order
+  const float4* nodes;     // [4*(T-1)] or 1 node for T == 1
+  const float4* mat;       // [2*nmesh]: (albedo, diffuse), (specular, transmission, ior, 0)
+  int32_t ntri;
+  int32_t nnodes;
+};
+
+struct Ray {
+  v3 o, d, inv;
+  int kx, ky, kz;
+  float Sx, Sy, Sz;
+};
+__device__ __forceinline__ void ray_prep(Ray& r, v3 o, v3 d) {
+  r.o = o;
+  r.d = d;
+  float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+  int kz = ax > ay ? (ax > az ? 0 : 2) : (ay > az ? 1 : 2);
+  int kx = kz + 1;
+  if (kx == 3) kx = 0;
+  int ky = kx + 1;
+  if (ky == 3) ky = 0;
+  const float dkz = comp(d, kz);
+  if (dkz < 0.0f) {
+    int t = kx;
+    kx = ky;
+    ky = t;
+  }
+  r.kx = kx;
+  r.ky = ky;
+  r.kz = kz;
+  r.Sx = comp(d, kx) / dkz;
+  r.Sy = comp(d, ky) / dkz;
+  r.Sz = 1.0f / dkz;
+  float cx = fabsf(d.x) < 1e-20f ? copysignf(1e-20f, d.x) : d.x;
+  float cy = fabsf(d.y) < 1e-20f ? copysignf(1e-20f, d.y) : d.y;
+  float cz = fabsf(d.z) < 1e-20f ? copysignf(1e-20f, d.z) : d.z;
+  r.inv = {1.0f / cx, 1.0f / cy, 1.0f / cz};
+}
+
+// Watertight ray/triangle (Woop, Benthin, Wald 2013): stands in for OptiX's
+// built-in triangle intersection (every optixTrace / owl::traceRay).
+__device__ __forceinline__ bool wt_hit(const float4 a, const float4 b, const float4 c, const Ray& r,
+                                       float& tout) {
+  const float A[3] = {a.x - r.o.x, a.y - r.o.y, a.z - r.o.z};
+  const float B[3] = {b.x - r.o.x, b.y - r.o.y, b.z - r.o.z};
+  const float C[3] = {c.x - r.o.x, c.y - r.o.y, c.z - r.o.z};
+  const float Akz = r.kz == 0 ? A[0] : (r.kz == 1 ? A[1] : A[2]);
+  const float Bkz = r.kz == 0 ? B[0] : (r.kz == 1 ? B[1] : B[2]);
+  const float Ckz = r.kz == 0 ? C[0] : (r.kz == 1 ? C[1] : C[2]);
+  const float Akx = r.kx == 0 ? A[0] : (r.kx == 1 ? A[1] : A[2]);
+  const float Bkx = r.kx == 0 ? B[0] : (r.kx == 1 ? B[1] : B[2]);
+  const float Ckx = r.kx == 0 ? C[0] : (r.kx == 1 ? C[1] : C[2]);
+  const float Aky = r.ky == 0 ? A[0] : (r.ky == 1 ? A[1] : A[2]);
+  const float Bky = r.ky == 0 ? B[0] : (r.ky == 1 ? B[1] : B[2]);
+  const float Cky = r.ky == 0 ? C[0] : (r.ky == 1 ? C[1] : C[2]);
+  const float Ax = Akx - r.Sx * Akz, Ay = Aky - r.Sy * Akz;
+  const float Bx = Bkx - r.Sx * Bkz, By = Bky - r.Sy * Bkz;
+  const float Cx = Ckx - r.Sx * Ckz, Cy = Cky - r.Sy * Ckz;
+  float U = Cx * By - Cy * Bx;
+  float V = Ax * Cy - Ay * Cx;
+  float W = Bx * Ay - By * Ax;
+  if (U == 0.0f || V == 0.0f || W == 0.0f) {
+    double CxBy = (double)Cx * (double)By, CyBx = (double)Cy * (double)Bx;
+    U = (float)(CxBy - CyBx);
+    double AxCy = (double)Ax * (double)Cy, AyCx = (double)Ay * (double)Cx;
+    V = (float)(AxCy - AyCx);
+    double BxAy = (double)Bx * (double)Ay, ByAx = (double)By * (double)Ax;
+    W = (float)(BxAy - ByAx);
+  }
+  if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
+  const float det = U + V + W;
+  if (det == 0.0f) return false;
+  const float Az = r.Sz * Akz, Bz = r.Sz * Bkz, Cz = r.Sz * Ckz;
+  const float T = U * Az + V * Bz + W * Cz;
+  tout = T / det;
+  return true;
+}
+
+// slab test for one box given as (x0,x1,y0,y1,z0,z1)
+__device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, float z0, float z1, const Ray& r,
+                                     float tmin, float tmax) {
+  const float t0x = (x0 - r.o.x) * r.inv.x, t1x = (x1 - r.o.x) * r.inv.x;
+  const float t0y = (y0 - r.o.y) * r.inv.y, t1y = (y1 - r.o.y) * r.inv.y;
+  const float t0z = (z0 - r.o.z) * r.inv.z, t1z = (z1 - r.o.z) * r.inv.z;
+  const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+  const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
+  return tn <= tf;
+}
+
+constexpr int kStackDepth = 64;
+
+struct HitInfo {
+  float t;
+  int32_t slot;   // triangle slot (leaf order) or -1
+  int32_t gid;    // global triangle index (tie-break key)
+};
+
+// Closest hit in (tmin, tmax): argmin (t, global triangle index). `stack`
+// points at this lane's column of an LDS stack laid out [depth][blockDim].
+template <bool ANY>
+__device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
+                                            int stride, int* overflow) {
+  HitInfo h{tmax, -1, -1};
+  if (S.ntri <= 0) return h;
+  int sp = 0;
+  int node = 0;
+  for (;;) {
+    const float4 n0 = S.nodes[4 * node + 0];
+    const float4 n1 = S.nodes[4 * node + 1];
+    const float4 n2 = S.nodes[4 * node + 2];
+    const int4 n3 = *reinterpret_cast<const int4*>(&S.nodes[4 * node + 3]);
+    const float lim = (ANY || h.slot < 0) ? tmax * 1.00001f : h.t * 1.00001f;
+    const bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, tmin, lim);
+    const bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, tmin, lim);
+    int next = -1;
+    int cand[2] = {hl ? n3.x : INT32_MAX, hr ? n3.y : INT32_MAX};
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const int ch = cand[c];
+      if (ch == INT32_MAX) continue;
+      if (ch < 0) {
+        const int slot = ~ch;
+        const float4 a = S.tri[3 * slot + 0];
+        const float4 b = S.tri[3 * slot + 1];
+        const float4 cc = S.tri[3 * slot + 2];
+        float t;
+        if (wt_hit(a, b, cc, r, t) && t > tmin && t < tmax) {
+          const int gid = __float_as_int(cc.w);
+          if (ANY) {
+            h.t = t;
+            h.slot = slot;
+            h.gid = gid;
+            return h;
+          }
+          if (h.slot < 0 || t < h.t || (t == h.t && gid < h.gid)) {
+            h.t = t;
+            h.slot = slot;
+            h.gid = gid;
+          }
+        }
+      } else if (next < 0) {
+        next = ch;
+      } else {
+        if (sp < kStackDepth) {
+          stack[sp * stride] = ch;
+          sp++;
+        } else {
+          *overflow = 1;
+        }
+      }
+    }
+    if (next >= 0) {
+      node = next;
+      continue;
+    }
+    if (sp == 0) break;
+    sp--;
+    node = stack[sp * stride];
+  }
+  return h;
+}
+
+__device__ __forceinline__ v3 tri_normal(const DevScene& S, int slot) {
+  const float4 a = S.tri[3 * slot + 0];
+  const float4 b = S.tri[3 * slot + 1];
+  const float4 c = S.tri[3 * slot + 2];
+  const v3 A = {a.x, a.y, a.z}, B = {b.x, b.y, b.z}, C = {c.x, c.y, c.z};
+  return normalize(cross(sub(B, A), sub(C, A)));
+}
+
+}  // namespace pmd

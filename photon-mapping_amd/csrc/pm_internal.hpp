@@ -1,0 +1,65 @@
+// pm_internal.hpp — handle layouts and kernel-launch entry points shared by the
+// translation units of libpm_hip.so (not part of the public C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/pm.h"
+#include "pm_device.hpp"
+#include "prims.hpp"
+
+// Device-resident scene: triangles in BVH leaf order + LBVH2 nodes + materials.
+struct pm_scene {
+  pmd::DevBuf<float4> tri;      // 3 per triangle
+  pmd::DevBuf<float4> nodes;    // 4 per internal node
+  pmd::DevBuf<float4> mat;      // 2 per mesh
+  pmd::DevBuf<int32_t> overflow;
+  int32_t ntri = 0, nnodes = 0, nmesh = 0, depth = 0;
+  pm_box bounds{};
+  std::vector<pm_material> host_mat;
+  pmd::DevScene view() const {
+    pmd::DevScene s;
+    s.tri = tri.p;
+    s.nodes = nodes.p;
+    s.mat = mat.p;
+    s.ntri = ntri;
+    s.nnodes = nnodes;
+    return s;
+  }
+};
+
+// Photon map: left-balanced kd-tree nodes (x, y, z, bits(orig<<2 | dim)) in
+// kd order + gather payload (color.xyz, power) in ORIGINAL order.
+struct pm_photon_map {
+  pmd::DevBuf<float4> nodes;
+  pmd::DevBuf<float4> payload;
+  int64_t n = 0;
+};
+
+namespace pmd {
+
+// phase timers (pm_last_phase_us)
+enum Phase { PH_TRACE = 0, PH_COMPACT = 1, PH_KDBUILD = 2, PH_PATHS = 3, PH_GATHER = 4, PH_RESOLVE = 5, PH_BVH = 6,
+             PH_COUNT = 7 };
+struct PhaseTimer {
+  hipEvent_t a = nullptr, b = nullptr;
+  hipStream_t s = nullptr;
+  int phase;
+  PhaseTimer(int ph, hipStream_t st);
+  ~PhaseTimer();
+};
+void record_phase_us(int phase, double us);
+
+hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& tri_host, hipStream_t s);
+
+// Core left-balanced kd-tree build over elements (x, y, z, bits(orig)).
+// Writes nodes[t] = (x, y, z, bits(orig << 2 | dim)).
+hipError_t kd_build(const float4* d_elems, int64_t n, float4* d_nodes, hipStream_t s);
+
+// K = 50 gather (gatherPhotons) for a batch of queries.
+hipError_t launch_gather(const pm_photon_map* m, const float4* d_query /*pos, brdf*/, int64_t nq,
+                         float4* d_out, hipStream_t s);
+
+}  // namespace pmd

@@ -1,0 +1,258 @@
+// prims.hip — caching allocator, exclusive scan, stable radix sort (gfx950).
+#include <map>
+#include <mutex>
+#include <unordered_map>
+
+#include "prims.hpp"
+
+namespace pmd {
+
+// ------------------------------------------------------------ allocator
+namespace {
+std::mutex g_mu;
+std::multimap<size_t, void*> g_free;           // size -> block
+std::unordered_map<void*, size_t> g_live;      // block -> size
+size_t round_up(size_t b) {
+  size_t r = 256;
+  while (r < b) r <<= 1;
+  return r;
+}
+}  // namespace
+
+void* dev_alloc(size_t bytes) {
+  const size_t sz = round_up(bytes ? bytes : 1);
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_free.find(sz);
+    if (it != g_free.end()) {
+      void* p = it->second;
+      g_free.erase(it);
+      g_live[p] = sz;
+      return p;
+    }
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, sz) != hipSuccess) {
+    (void)hipGetLastError();
+    dev_cache_trim();
+    if (hipMalloc(&p, sz) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_live[p] = sz;
+  return p;
+}
+
+void dev_free(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_live.find(p);
+  if (it == g_live.end()) return;
+  g_free.emplace(it->second, p);
+  g_live.erase(it);
+}
+
+void dev_cache_trim() {
+  (void)hipDeviceSynchronize();
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& kv : g_free) (void)hipFree(kv.second);
+  g_free.clear();
+}
+
+// ------------------------------------------------------------ scan
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanBlock * kScanItems;
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// block exclusive scan of one value per thread; returns exclusive prefix, *tot = block total
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* sh, T& tot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  T inc = wave_incl_scan(v);
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T run = 0;
+    for (int i = 0; i < kScanBlock / 64; i++) {
+      T t = sh[i];
+      sh[i] = run;
+      run += t;
+    }
+    sh[kScanBlock / 64] = run;
+  }
+  __syncthreads();
+  T r = inc - v + sh[w];
+  tot = sh[kScanBlock / 64];
+  __syncthreads();
+  return r;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const T* in, int64_t n, T* bsum) {
+  __shared__ T sh[kScanBlock / 64 + 1];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile;
+  T acc = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++) {
+    int64_t i = base + (int64_t)k * kScanBlock + threadIdx.x;
+    if (i < n) acc += in[i];
+  }
+  T tot;
+  (void)block_excl_scan<T>(acc, sh, tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScanBlock) void k_scan_down(const T* in, T* out, int64_t n, const T* boff, T* total,
+                                                          int nblocks) {
+  __shared__ T sh[kScanBlock / 64 + 1];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile;
+  // each thread owns kScanItems consecutive elements
+  T v[kScanItems];
+  T acc = 0;
+  const int64_t mine = base + (int64_t)threadIdx.x * kScanItems;
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++) {
+    int64_t i = mine + k;
+    v[k] = i < n ? in[i] : (T)0;
+    acc += v[k];
+  }
+  T tot;
+  T pre = block_excl_scan<T>(acc, sh, tot) + (boff ? boff[blockIdx.x] : (T)0);
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++) {
+    int64_t i = mine + k;
+    if (i < n) out[i] = pre;
+    pre += v[k];
+  }
+  if (total && blockIdx.x == nblocks - 1 && threadIdx.x == kScanBlock - 1) *total = pre;
+}
+
+template <typename T>
+static hipError_t scan_impl(const T* in, T* out, int64_t n, T* total, hipStream_t s) {
+  if (n <= 0) {
+    if (total) PM_HIP_TRY(hipMemsetAsync(total, 0, sizeof(T), s));
+    return hipSuccess;
+  }
+  const int nb = (int)((n + kScanTile - 1) / kScanTile);
+  if (nb == 1) {
+    k_scan_down<T><<<1, kScanBlock, 0, s>>>(in, out, n, nullptr, total, 1);
+    return hipGetLastError();
+  }
+  DevBuf<T> bsum(nb), boff(nb);
+  if (!bsum.p || !boff.p) return hipErrorOutOfMemory;
+  k_scan_reduce<T><<<nb, kScanBlock, 0, s>>>(in, n, bsum.p);
+  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(scan_impl<T>(bsum.p, boff.p, nb, nullptr, s));
+  k_scan_down<T><<<nb, kScanBlock, 0, s>>>(in, out, n, boff.p, total, nb);
+  return hipGetLastError();
+}
+
+hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total, hipStream_t s) {
+  return scan_impl<uint32_t>(in, out, n, total, s);
+}
+hipError_t exclusive_scan_u64(const uint64_t* in, uint64_t* out, int64_t n, uint64_t* total, hipStream_t s) {
+  return scan_impl<uint64_t>(in, out, n, total, s);
+}
+
+// ------------------------------------------------------------ radix sort
+// 8-bit digits; tile = 256 threads x 8 rounds. Histogram -> digit-major scan
+// -> stable scatter with wave64 ballot multi-split ranking.
+constexpr int kSortBlock = 256;
+constexpr int kSortRounds = 8;
+constexpr int kSortTile = kSortBlock * kSortRounds;
+
+__global__ __launch_bounds__(kSortBlock) void k_sort_hist(const uint32_t* keys, int64_t n, int shift,
+                                                          uint32_t* hist, int nblocks) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+#pragma unroll
+  for (int r = 0; r < kSortRounds; r++) {
+    int64_t i = base + (int64_t)r * kSortBlock + threadIdx.x;
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const uint32_t* keys, const uint32_t* vals,
+                                                             uint32_t* okeys, uint32_t* ovals, int64_t n, int shift,
+                                                             const uint32_t* hoff, int nblocks) {
+  __shared__ uint32_t running[256];
+  __shared__ uint32_t wcnt[kSortBlock / 64][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  running[threadIdx.x] = hoff[(int64_t)threadIdx.x * nblocks + blockIdx.x];
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  for (int r = 0; r < kSortRounds; r++) {
+#pragma unroll
+    for (int k = 0; k < kSortBlock / 64; k++) wcnt[k][threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t i = base + (int64_t)r * kSortBlock + threadIdx.x;
+    const bool valid = i < n;
+    uint32_t key = valid ? keys[i] : 0u;
+    uint32_t val = valid ? vals[i] : 0u;
+    const uint32_t dg = (key >> shift) & 0xFF;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const uint64_t bal = __ballot((dg >> b) & 1);
+      peers &= ((dg >> b) & 1) ? bal : ~bal;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & lt_mask);
+    if (valid && rank == 0) wcnt[w][dg] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = running[dg] + rank;
+      for (int k = 0; k < w; k++) pos += wcnt[k][dg];
+      okeys[pos] = key;
+      ovals[pos] = val;
+    }
+    __syncthreads();
+    uint32_t add = 0;
+#pragma unroll
+    for (int k = 0; k < kSortBlock / 64; k++) add += wcnt[k][threadIdx.x];
+    running[threadIdx.x] += add;
+    __syncthreads();
+  }
+}
+
+hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, int64_t n, int end_bit, hipStream_t s) {
+  if (n <= 1) return hipSuccess;
+  const int nb = (int)((n + kSortTile - 1) / kSortTile);
+  DevBuf<uint32_t> k2(n), v2(n), hist((size_t)256 * nb), hoff((size_t)256 * nb);
+  if (!k2.p || !v2.p || !hist.p || !hoff.p) return hipErrorOutOfMemory;
+  uint32_t *ka = keys, *va = vals, *kb = k2.p, *vb = v2.p;
+  int passes = 0;
+  for (int shift = 0; shift < end_bit; shift += 8, passes++) {
+    k_sort_hist<<<nb, kSortBlock, 0, s>>>(ka, n, shift, hist.p, nb);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(exclusive_scan_u32(hist.p, hoff.p, (int64_t)256 * nb, nullptr, s));
+    k_sort_scatter<<<nb, kSortBlock, 0, s>>>(ka, va, kb, vb, n, shift, hoff.p, nb);
+    PM_HIP_TRY(hipGetLastError());
+    uint32_t* t = ka; ka = kb; kb = t;
+    t = va; va = vb; vb = t;
+  }
+  if (passes & 1) {
+    PM_HIP_TRY(hipMemcpyAsync(keys, ka, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    PM_HIP_TRY(hipMemcpyAsync(vals, va, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  }
+  return hipSuccess;
+}
+
+}  // namespace pmd

@@ -1,0 +1,63 @@
+// prims.hpp — device primitives shared by the hot-path kernels (gfx950):
+// stream-ordered caching allocator, exclusive scan (u32/u64), stable LSD radix
+// sort of (u32 key, u32 value) pairs. Hand-written HIP, wave64 idioms.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstddef>
+
+namespace pmd {
+
+// Caching device allocator: freed blocks are kept and reused (stream-ordered
+// reuse on the library's single stream), so timed loops do not hipMalloc.
+void* dev_alloc(size_t bytes);
+void dev_free(void* p);
+void dev_cache_trim();
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  explicit DevBuf(size_t count) { alloc(count); }
+  ~DevBuf() { reset(); }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  void alloc(size_t count) {
+    reset();
+    n = count;
+    p = count ? static_cast<T*>(dev_alloc(count * sizeof(T))) : nullptr;
+  }
+  void reset() {
+    if (p) dev_free(p);
+    p = nullptr;
+    n = 0;
+  }
+  T* get() const { return p; }
+};
+
+// out[i] = sum_{j<i} in[j]; if total != nullptr, *total (device) = sum of all.
+hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total, hipStream_t s);
+hipError_t exclusive_scan_u64(const uint64_t* in, uint64_t* out, int64_t n, uint64_t* total, hipStream_t s);
+
+// Stable LSD radix sort on key bits [0, end_bit). Sorted data ends in keys/vals.
+hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, int64_t n, int end_bit, hipStream_t s);
+
+// float -> uint32 whose unsigned order == float order, with -0 == +0.
+__host__ __device__ inline uint32_t orderable_key(float f) {
+  if (f == 0.0f) f = 0.0f;
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+inline int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
+
+}  // namespace pmd
+
+#define PM_HIP_TRY(expr)                         \
+  do {                                           \
+    hipError_t _e = (expr);                      \
+    if (_e != hipSuccess) return _e;             \
+  } while (0)

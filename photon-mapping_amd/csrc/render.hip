@@ -1,0 +1,445 @@
+// render.hip — final gather render for gfx950 (stage 2).
+//
+// Restates simpleRayGen / tracePath / ray_colour (ray-tracer/cuda/deviceCode.cu:
+// 25-231) and reflect_or_refract_ray / calculate_refracted / specularBrdf
+// (ray-tracer/cuda/shading.h:20-91) as a wavefront pipeline:
+//   1. k_count_paths  per pixel: camera path only (no shadow / diffuse rays)
+//                     -> number of ray_colour calls (path vertices). RNG use of
+//                     the 20 diffuse samples is replayed (it is independent of
+//                     what the diffuse rays hit), so the path is exact.
+//   2. scan           -> deterministic vertex slots per pixel.
+//   3. k_paths        per pixel: full path with shadow rays and the 20 diffuse
+//                     rays; writes per-vertex records and one caustic + up to 20
+//                     global gather queries per vertex into fixed slots.
+//   4. compaction of valid queries, k_gather (knn.hip) per query.
+//   5. k_resolve      per pixel: replays ray_colour's colour arithmetic in the
+//                     reference's order with the gathered radiance.
+// Gathers never steer control flow, so this is bitwise the megakernel result.
+// Reference UB is defined as in SURVEY §5.1-18: per-pixel hit record and the
+// diffuse rays' hit records are zero-initialised; a miss keeps the stale record.
+#include <algorithm>
+#include <cstring>
+
+#include "pm_internal.hpp"
+
+namespace pmd {
+
+constexpr int kRBlock = 128;
+constexpr uint32_t VF_MISS = 1u, VF_LAST = 2u;
+
+struct LightR {
+  float4 pos;   // xyz, power (float)
+  float4 rgb;
+};
+
+struct RenderArgs {
+  int32_t W, H, spp, depth;
+  int32_t tile_rank, tile_count, tiles_x, my_tiles;
+  v3 cam_pos, d00, du, dv, sky;
+  const LightR* lights;
+  int32_t nl;
+};
+
+struct HitRec {
+  v3 hitpoint, normal;
+  float4 m0, m1;   // (albedo, diffuse), (specular, transmission, ior, 0)
+};
+
+__device__ __forceinline__ bool pixel_of(const RenderArgs& A, int64_t tid, int& px, int& py) {
+  const int64_t lt = tid >> 8;
+  if (lt >= A.my_tiles) return false;
+  const int64_t tile = (int64_t)A.tile_rank + lt * A.tile_count;
+  const int ty = (int)(tile / A.tiles_x), tx = (int)(tile % A.tiles_x);
+  const int p = (int)(tid & 255);
+  px = tx * 16 + (p & 15);
+  py = ty * 16 + (p >> 4);
+  return px < A.W && py < A.H;
+}
+
+// closestHit (deviceCode.cu:233-253)
+__device__ __forceinline__ bool trace_closest(const DevScene& S, v3 o, v3 d, float tmin, float tmax, HitRec& hr,
+                                              int* st, int* overflow) {
+  Ray r;
+  ray_prep(r, o, d);
+  const HitInfo h = traverse<false>(S, r, tmin, tmax, st, kRBlock, overflow);
+  if (h.slot < 0) return false;
+  const int mesh = __float_as_int(S.tri[3 * h.slot].w);
+  hr.m0 = S.mat[2 * mesh];
+  hr.m1 = S.mat[2 * mesh + 1];
+  hr.hitpoint = add(o, mulf(d, h.t));
+  const v3 n = tri_normal(S, h.slot);
+  hr.normal = dot(d, n) < 0.f ? n : neg(n);
+  hr.normal = normalize(hr.normal);
+  return true;
+}
+
+// shading.h:20-55 (Random by value)
+__device__ __forceinline__ v3 calculate_refracted(const HitRec& hr, v3 rd, v3 n, uint32_t rng) {
+  v3 outward, refracted = {0.f, 0.f, 0.f};
+  float ni, R, cosine;
+  const float ior = hr.m1.z;
+  if (dot(rd, n) > 0.f) {
+    outward = neg(n);
+    ni = ior;
+    cosine = dot(rd, n);
+    cosine = sqrtf(1.f - ior * ior * (1.f - cosine * cosine));
+  } else {
+    outward = n;
+    ni = 1.f / ior;
+    cosine = -dot(rd, n);
+  }
+  if (refract_uv(rd, outward, ni, refracted))
+    R = schlick(cosine, ior);
+  else
+    R = 1.f;
+  if (lcg_next(rng) < R) return reflect(rd, n);
+  return refracted;
+}
+// shading.h:57-80 (Random by value)
+__device__ __forceinline__ v3 reflect_or_refract(const HitRec& hr, v3 rd, v3 n, uint32_t rng, bool& absorbed,
+                                                 float& coef) {
+  absorbed = false;
+  const float r = lcg_next(rng);
+  if (r < hr.m1.x) {
+    coef = hr.m1.x;
+    return reflect(rd, n);
+  }
+  if (r < hr.m1.x + hr.m1.y) {
+    coef = hr.m1.y;
+    return calculate_refracted(hr, rd, n, rng);
+  }
+  coef = 0.f;
+  absorbed = true;
+  return {0.f, 0.f, 0.f};
+}
+
+// deviceCode.cu:112-120: the RNG use of one diffuse sample (direction only)
+__device__ __forceinline__ v3 diffuse_direction(v3 normal_at_hit, uint32_t& rng) {
+  const v3 n = normalize(normal_at_hit);
+  v3 rv, rdir;
+  do {
+    rv = random_unit_vector(rng);
+    rdir = add(n, rv);
+  } while (near_zero(rdir));
+  return normalize(rdir);
+}
+
+__device__ __forceinline__ v3 camera_dir(const RenderArgs& A, int px, int py, uint32_t& rng) {
+  const float ex = lcg_next(rng);   // vec2f(rnd(), rnd()) evaluated left to right
+  const float ey = lcg_next(rng);
+  const float su = ((float)px + ex) / (float)A.W;
+  const float sv = ((float)py + ey) / (float)A.H;
+  return normalize(add(add(A.d00, smul(su, A.du)), smul(sv, A.dv)));
+}
+
+__global__ __launch_bounds__(kRBlock) void k_count_paths(DevScene S, RenderArgs A, uint32_t* cnt, int* overflow) {
+  __shared__ int stack[kStackDepth * kRBlock];
+  const int64_t tid = (int64_t)blockIdx.x * kRBlock + threadIdx.x;
+  int px, py;
+  if (!pixel_of(A, tid, px, py)) {
+    if ((tid >> 8) < A.my_tiles) cnt[tid] = 0;
+    return;
+  }
+  int* st = stack + threadIdx.x;
+  uint32_t rng = lcg_init((uint32_t)px, (uint32_t)py);
+  HitRec hr;
+  hr.hitpoint = hr.normal = {0.f, 0.f, 0.f};
+  hr.m0 = hr.m1 = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint32_t V = 0;
+  for (int s = 0; s < A.spp; s++) {
+    v3 ro = A.cam_pos;
+    v3 rd = camera_dir(A, px, py, rng);
+    for (int d = 0; d < A.depth; d++) {
+      V++;
+      if (trace_closest(S, ro, rd, kEPS, kINFTY, hr, st, overflow)) {
+        const float diffuse_brdf = hr.m0.w / kPI;
+        for (int k = 0; k < kNumDiffuseSamples && diffuse_brdf > 0.f; k++) (void)diffuse_direction(hr.normal, rng);
+      }
+      bool absorbed;
+      float coef;
+      const v3 od = reflect_or_refract(hr, rd, hr.normal, rng, absorbed, coef);
+      if (absorbed) break;
+      ro = hr.hitpoint;
+      rd = od;
+    }
+  }
+  cnt[tid] = V;
+}
+
+struct PathOut {
+  float4* vdirect;    // direct term (or sky colour for a miss)
+  float4* vatt;       // attenuation at this vertex
+  float4* valb;       // albedo at this vertex
+  uint32_t* vflags;
+  float4* cq;         // caustic query (hitpoint, diffuse_brdf)
+  uint32_t* cvalid;
+  float4* gq;         // [20 * v + j] global query (hitpoint, brdf)
+  float4* galb;       // [20 * v + j] albedo of the diffuse hit
+  uint32_t* gvalid;
+  unsigned long long* rays;
+};
+
+__global__ __launch_bounds__(kRBlock) void k_paths(DevScene S, RenderArgs A, const uint32_t* voff, PathOut O,
+                                                   int* overflow) {
+  __shared__ int stack[kStackDepth * kRBlock];
+  const int64_t tid = (int64_t)blockIdx.x * kRBlock + threadIdx.x;
+  int px, py;
+  if (!pixel_of(A, tid, px, py)) return;
+  int* st = stack + threadIdx.x;
+  uint32_t rng = lcg_init((uint32_t)px, (uint32_t)py);
+  HitRec hr;
+  hr.hitpoint = hr.normal = {0.f, 0.f, 0.f};
+  hr.m0 = hr.m1 = make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t v = voff[tid];
+  uint32_t nrays = 0;
+  for (int s = 0; s < A.spp; s++) {
+    v3 ro = A.cam_pos;
+    v3 rd = camera_dir(A, px, py, rng);
+    v3 att = {1.f, 1.f, 1.f};
+    for (int d = 0; d < A.depth; d++, v++) {
+      nrays++;
+      const bool hit = trace_closest(S, ro, rd, kEPS, kINFTY, hr, st, overflow);
+      O.vatt[v] = make_float4(att.x, att.y, att.z, 0.f);
+      uint32_t fl = 0;
+      if (!hit) {
+        fl |= VF_MISS;
+        O.vdirect[v] = make_float4(A.sky.x, A.sky.y, A.sky.z, 0.f);
+        O.cvalid[v] = 0;
+#pragma unroll 1
+        for (int j = 0; j < kNumDiffuseSamples; j++) O.gvalid[(int64_t)v * kNumDiffuseSamples + j] = 0;
+      } else {
+        const v3 albedo = {hr.m0.x, hr.m0.y, hr.m0.z};
+        const float diffuse_brdf = hr.m0.w / kPI;
+        v3 direct = {0.f, 0.f, 0.f};
+        for (int l = 0; l < A.nl; l++) {
+          const LightR L = A.lights[l];
+          const v3 org = hr.hitpoint;
+          v3 ldir = sub(v3{L.pos.x, L.pos.y, L.pos.z}, org);
+          const float dist = norm3(ldir);
+          ldir = normalize(ldir);
+          const float ldn = dot(ldir, hr.normal);
+          if (ldn < 0.f) continue;
+          Ray r;
+          ray_prep(r, org, ldir);
+          nrays++;
+          const HitInfo sh = traverse<true>(S, r, kEPS, dist * (1.f - kEPS), st, kRBlock, overflow);
+          const float vis = sh.slot >= 0 ? 0.f : 1.f;
+          // specularBrdf (shading.h:82-91)
+          const float sb = near_zero(sub(reflect(ldir, hr.normal), rd)) ? hr.m1.x : 0.f;
+          const float pw = L.pos.w;
+          const float inv = 1.f / (dist * dist);
+          const float bs = diffuse_brdf + sb;
+          direct = add(direct, v3{vis * pw * ldn * inv * bs * L.rgb.x, vis * pw * ldn * inv * bs * L.rgb.y,
+                                  vis * pw * ldn * inv * bs * L.rgb.z});
+        }
+        const v3 dt = mulv(albedo, direct);
+        O.vdirect[v] = make_float4(dt.x, dt.y, dt.z, 0.f);
+        O.valb[v] = make_float4(albedo.x, albedo.y, albedo.z, 0.f);
+        O.cq[v] = make_float4(hr.hitpoint.x, hr.hitpoint.y, hr.hitpoint.z, diffuse_brdf);
+        O.cvalid[v] = 1;
+        for (int j = 0; j < kNumDiffuseSamples; j++) {
+          const int64_t gi = (int64_t)v * kNumDiffuseSamples + j;
+          uint32_t ok = 0;
+          if (diffuse_brdf > 0.f) {
+            const v3 rdir = diffuse_direction(hr.normal, rng);
+            HitRec dh;
+            nrays++;
+            if (trace_closest(S, hr.hitpoint, rdir, 3 * kEPS, kINFTY, dh, st, overflow) && dh.m0.w > 0.f) {
+              O.gq[gi] = make_float4(dh.hitpoint.x, dh.hitpoint.y, dh.hitpoint.z, dh.m0.w / kPI);
+              O.galb[gi] = make_float4(dh.m0.x, dh.m0.y, dh.m0.z, 0.f);
+              ok = 1;
+            }
+          }
+          O.gvalid[gi] = ok;
+        }
+      }
+      bool absorbed;
+      float coef;
+      const v3 od = reflect_or_refract(hr, rd, hr.normal, rng, absorbed, coef);
+      const bool last = absorbed || d == A.depth - 1;
+      if (last) fl |= VF_LAST;
+      O.vflags[v] = fl;
+      if (absorbed) {
+        v++;
+        break;
+      }
+      att = mulv(att, smul(coef, v3{hr.m0.x, hr.m0.y, hr.m0.z}));
+      ro = hr.hitpoint;
+      rd = od;
+    }
+  }
+  atomicAdd(O.rays, (unsigned long long)nrays);
+}
+
+__global__ void k_compact_q(const float4* q, const uint32_t* valid, const uint32_t* idx, int64_t n, float4* dense) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (valid[i]) dense[idx[i]] = q[i];
+}
+
+__global__ __launch_bounds__(256) void k_resolve(RenderArgs A, const uint32_t* voff, const uint32_t* cnt,
+                                                 PathOut O, const uint32_t* cidx, const float4* cres,
+                                                 const uint32_t* gidx, const float4* gres, uint32_t* rgba,
+                                                 float* rgb) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int px, py;
+  if (!pixel_of(A, tid, px, py)) return;
+  int64_t v = voff[tid];
+  const int64_t vend = v + cnt[tid];
+  v3 fc = {0.f, 0.f, 0.f};
+  for (int s = 0; s < A.spp && v < vend; s++) {
+    v3 colour = {0.f, 0.f, 0.f};
+    for (; v < vend;) {
+      const uint32_t fl = O.vflags[v];
+      const float4 a4 = O.vatt[v];
+      const v3 att = {a4.x, a4.y, a4.z};
+      v3 c;
+      if (fl & VF_MISS) {
+        const float4 sk = O.vdirect[v];
+        c = {sk.x, sk.y, sk.z};
+      } else {
+        const float4 c4 = cres[cidx[v]];
+        const v3 caustics = {c4.x, c4.y, c4.z};
+        v3 diffuse = {0.f, 0.f, 0.f};
+        for (int j = 0; j < kNumDiffuseSamples; j++) {
+          const int64_t gi = v * kNumDiffuseSamples + j;
+          if (!O.gvalid[gi]) continue;
+          const float4 g4 = gres[gidx[gi]];
+          const float4 al = O.galb[gi];
+          diffuse = add(diffuse, mulv(v3{g4.x, g4.y, g4.z}, v3{al.x, al.y, al.z}));
+        }
+        diffuse = divf(diffuse, (float)kNumDiffuseSamples);
+        const float4 ab = O.valb[v];
+        diffuse = mulv(diffuse, v3{ab.x, ab.y, ab.z});
+        const float4 d4 = O.vdirect[v];
+        c = {kDiffuseFactor * diffuse.x + kCausticsFactor * caustics.x + kDirectLightFactor * d4.x,
+             kDiffuseFactor * diffuse.y + kCausticsFactor * caustics.y + kDirectLightFactor * d4.y,
+             kDiffuseFactor * diffuse.z + kCausticsFactor * caustics.z + kDirectLightFactor * d4.z};
+      }
+      colour = add(colour, mulv(c, att));
+      v++;
+      if (fl & VF_LAST) break;
+    }
+    fc = add(fc, colour);
+  }
+  fc = mulf(fc, 1.f / (float)A.spp);
+  const int y = A.H - py;
+  if (y >= A.H) return;   // pixelID.y == 0 writes past the buffer in the reference: dropped
+  const int64_t ofs = (int64_t)px + (int64_t)A.W * y;
+  // owl make_rgba: clamp(int(f*256), 0, 255), alpha 0xff (v_cvt_i32_f32 saturates, NaN -> 0)
+  auto q = [](float f) -> uint32_t {
+    const float g = f * 256.f;
+    int i = (g == g) ? (int)fminf(fmaxf(g, -2147483648.f), 2147483520.f) : 0;
+    return (uint32_t)min(255, max(0, i));
+  };
+  rgba[ofs] = q(fc.x) | (q(fc.y) << 8) | (q(fc.z) << 16) | (0xFFu << 24);
+  if (rgb) {
+    rgb[3 * ofs] = fc.x;
+    rgb[3 * ofs + 1] = fc.y;
+    rgb[3 * ofs + 2] = fc.z;
+  }
+}
+
+hipError_t render_impl(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int nl,
+                       const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba, float* rgb,
+                       pm_render_stats* stats, hipStream_t s) {
+  RenderArgs A;
+  A.W = P->width;
+  A.H = P->height;
+  A.spp = P->samples_per_pixel;
+  A.depth = P->max_depth;
+  A.tile_rank = P->tile_count > 1 ? P->tile_rank : 0;
+  A.tile_count = P->tile_count > 1 ? P->tile_count : 1;
+  A.tiles_x = (A.W + 15) / 16;
+  const int tiles_y = (A.H + 15) / 16;
+  const int64_t ntiles = (int64_t)A.tiles_x * tiles_y;
+  A.my_tiles = (int32_t)(ntiles > A.tile_rank ? (ntiles - A.tile_rank + A.tile_count - 1) / A.tile_count : 0);
+  A.cam_pos = mk(P->camera.pos);
+  A.d00 = mk(P->camera.dir_00);
+  A.du = mk(P->camera.dir_du);
+  A.dv = mk(P->camera.dir_dv);
+  A.sky = mk(P->sky_colour);
+  A.nl = nl;
+  std::vector<LightR> lh(nl > 0 ? nl : 1);
+  for (int i = 0; i < nl; i++) {
+    lh[i].pos = make_float4(lights[i].pos.x, lights[i].pos.y, lights[i].pos.z, (float)lights[i].power);
+    lh[i].rgb = make_float4(lights[i].rgb.x, lights[i].rgb.y, lights[i].rgb.z, 0.f);
+  }
+  DevBuf<LightR> dl(lh.size());
+  if (!dl.p) return hipErrorOutOfMemory;
+  PM_HIP_TRY(hipMemcpyAsync(dl.p, lh.data(), sizeof(LightR) * lh.size(), hipMemcpyHostToDevice, s));
+  A.lights = dl.p;
+  const int64_t nthreads = (int64_t)A.my_tiles * 256;
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  if (nthreads == 0) return hipSuccess;
+  const DevScene S = sc->view();
+  DevBuf<uint32_t> cnt(nthreads), voff(nthreads), tot(1);
+  if (!cnt.p || !voff.p || !tot.p) return hipErrorOutOfMemory;
+  uint32_t V = 0;
+  {
+    PhaseTimer tm(PH_PATHS, s);
+    k_count_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, cnt.p, sc->overflow.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(exclusive_scan_u32(cnt.p, voff.p, nthreads, tot.p, s));
+    PM_HIP_TRY(hipMemcpyAsync(&V, tot.p, 4, hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+  }
+  const int64_t NV = V, NG = (int64_t)V * kNumDiffuseSamples;
+  DevBuf<float4> vdirect(NV), vatt(NV), valb(NV), cq(NV), gq(NG), galb(NG);
+  DevBuf<uint32_t> vflags(NV), cvalid(NV), gvalid(NG), cidx(NV), gidx(NG), ctot(1), gtot(1);
+  DevBuf<unsigned long long> rays(1);
+  if (NV > 0 && (!vdirect.p || !vatt.p || !valb.p || !cq.p || !gq.p || !galb.p || !vflags.p || !cvalid.p ||
+                 !gvalid.p || !cidx.p || !gidx.p))
+    return hipErrorOutOfMemory;
+  PathOut O{vdirect.p, vatt.p, valb.p, vflags.p, cq.p, cvalid.p, gq.p, galb.p, gvalid.p, rays.p};
+  uint32_t NC = 0, NGv = 0;
+  {
+    PhaseTimer tm(PH_PATHS, s);
+    PM_HIP_TRY(hipMemsetAsync(rays.p, 0, 8, s));
+    k_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, voff.p, O, sc->overflow.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(exclusive_scan_u32(cvalid.p, cidx.p, NV, ctot.p, s));
+    PM_HIP_TRY(exclusive_scan_u32(gvalid.p, gidx.p, NG, gtot.p, s));
+    PM_HIP_TRY(hipMemcpyAsync(&NC, ctot.p, 4, hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipMemcpyAsync(&NGv, gtot.p, 4, hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+  }
+  DevBuf<float4> cdense(NC), gdense(NGv), cres(NC), gres(NGv);
+  if ((NC && (!cdense.p || !cres.p)) || (NGv && (!gdense.p || !gres.p))) return hipErrorOutOfMemory;
+  {
+    PhaseTimer tm(PH_GATHER, s);
+    if (NV) {
+      k_compact_q<<<grid_for(NV, 256), 256, 0, s>>>(cq.p, cvalid.p, cidx.p, NV, cdense.p);
+      PM_HIP_TRY(hipGetLastError());
+      k_compact_q<<<grid_for(NG, 256), 256, 0, s>>>(gq.p, gvalid.p, gidx.p, NG, gdense.p);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    PM_HIP_TRY(launch_gather(cmap, cdense.p, NC, cres.p, s));
+    PM_HIP_TRY(launch_gather(gmap, gdense.p, NGv, gres.p, s));
+  }
+  {
+    PhaseTimer tm(PH_RESOLVE, s);
+    k_resolve<<<grid_for(nthreads, 256), 256, 0, s>>>(A, voff.p, cnt.p, O, cidx.p, cres.p, gidx.p, gres.p, rgba,
+                                                      rgb);
+    PM_HIP_TRY(hipGetLastError());
+  }
+  unsigned long long nr = 0;
+  PM_HIP_TRY(hipMemcpyAsync(&nr, rays.p, 8, hipMemcpyDeviceToHost, s));
+  PM_HIP_TRY(hipStreamSynchronize(s));
+  if (stats) {
+    int64_t px = 0;
+    for (int64_t t = 0; t < A.my_tiles; t++) {
+      const int64_t tile = A.tile_rank + t * A.tile_count;
+      const int ty = (int)(tile / A.tiles_x), tx = (int)(tile % A.tiles_x);
+      px += (int64_t)std::min(16, A.W - tx * 16) * std::min(16, A.H - ty * 16);
+    }
+    stats->pixels = px;
+    stats->path_vertices = NV;
+    stats->caustic_queries = NC;
+    stats->global_queries = NGv;
+    stats->rays = (int64_t)nr;
+  }
+  return hipSuccess;
+}
+
+}  // namespace pmd

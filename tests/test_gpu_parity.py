@@ -1,0 +1,294 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on the
+same seeded inputs. Integer / index results and the arithmetic-spec floats are
+compared bit for bit; the image is compared with the north-star tolerance
+(L_inf <= 1e-3 per channel on the [0,1]-clamped colour) and the exact-match
+fraction is asserted too."""
+import numpy as np
+import pytest
+
+import conftest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import pm_amd
+    if not torch.cuda.is_available() or pm_amd.device_count() == 0:
+        pytest.fail("GPU tests need a visible MI355X (HIP device)")
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def random_rays(n, lo, hi, seed, tmin=1e-3, tmax=1e10):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r = np.zeros((n, 8), np.float32)
+    r[:, 0:3] = o
+    r[:, 3] = tmin
+    r[:, 4:7] = d
+    r[:, 7] = tmax
+    return r
+
+
+def _scene_pair(meshes, use_bvh=True):
+    import oracle
+    import pm_amd
+    return pm_amd.Scene(meshes), oracle.Scene(meshes, use_bvh=use_bvh)
+
+
+@pytest.mark.parametrize("which", ["cornell", "sphere"])
+def test_intersect_bitwise(which, request):
+    meshes, _ = request.getfixturevalue(which)
+    gs, os_ = _scene_pair(meshes, use_bvh=(which != "cornell"))
+    rays = random_rays(20000, [-25, -5, -25], [25, 45, 25], seed=1)
+    # include axis-aligned and boundary-grazing rays
+    rays[:500, 4:7] = np.eye(3, dtype=np.float32)[np.arange(500) % 3]
+    hg = gs.intersect(torch.from_numpy(rays).cuda()).cpu().numpy()
+    ho = os_.intersect(rays)
+    assert np.array_equal(hg[:, 1:], ho[:, 1:]), "hit ids differ"
+    assert np.array_equal(hg[:, 0], ho[:, 0]), "hit t differs (bits)"
+    assert (ho[:, 1] >= 0).mean() > 0.5
+
+
+def test_occluded(cornell):
+    meshes, _ = cornell
+    gs, os_ = _scene_pair(meshes, use_bvh=False)
+    rays = random_rays(20000, [-19, 1, -19], [19, 39, 19], seed=2, tmax=15.0)
+    og = gs.occluded(torch.from_numpy(rays).cuda()).cpu().numpy()
+    oo = os_.occluded(rays)
+    assert np.array_equal(og, oo)
+    assert 0 < og.mean() < 1
+
+
+def test_scene_stats(sphere):
+    import pm_amd
+    meshes, _ = sphere
+    s = pm_amd.Scene(meshes).stats()
+    assert s.num_triangles == sum(len(m.indices) for m in meshes)
+    assert s.num_nodes == s.num_triangles - 1
+    assert 0 < s.max_depth <= 64
+
+
+@pytest.mark.parametrize("which,casted", [("cornell", 10000), ("sphere", 100000)])
+@pytest.mark.parametrize("caustics", [False, True])
+def test_trace_bitwise(which, casted, caustics, request):
+    import oracle
+    import pm_amd
+    meshes, lights = request.getfixturevalue(which)
+    gs, os_ = _scene_pair(meshes)
+    pg = pm_amd.run_point_light_ray_gen(gs, lights, casted, 10, caustics).cpu().numpy()
+    po = oracle.trace(os_, lights, casted, 10, caustics)
+    assert pg.shape == po.shape, (pg.shape, po.shape)
+    assert np.array_equal(_bits(pg), _bits(po))
+    assert len(pg) > 0
+
+
+def test_trace_shards_concatenate(cornell):
+    import pm_amd
+    meshes, lights = cornell
+    gs = pm_amd.Scene(meshes)
+    full = pm_amd.run_normal(gs, lights, 30000, 10).cpu().numpy()
+    parts = [pm_amd.run_normal(gs, lights, 30000, 10, shard_rank=r, shard_count=3).cpu().numpy() for r in range(3)]
+    assert np.array_equal(_bits(np.concatenate(parts)), _bits(full))
+
+
+def test_trace_capacity_error(cornell):
+    import pm_amd
+    meshes, lights = cornell
+    gs = pm_amd.Scene(meshes)
+    small = torch.empty((10, 10), dtype=torch.float32, device="cuda")
+    with pytest.raises(pm_amd.PMError) as e:
+        pm_amd.run_normal(gs, lights, 10000, 10, out=small)
+    assert e.value.status == pm_amd.PM_ERR_CAPACITY
+
+
+def test_trace_edge_cases(cornell):
+    import pm_amd
+    meshes, lights = cornell
+    gs = pm_amd.Scene(meshes)
+    assert pm_amd.run_normal(gs, lights, 10, 10).shape[0] == 0          # casted < sum P -> 0 photons
+    assert pm_amd.run_normal(gs, lights, 10000, 1).shape[0] == 0        # max_depth 1: no i > 0 bounce
+    assert pm_amd.run_normal(gs, lights, 10000, 0).shape[0] == 0
+    assert pm_amd.run_normal(gs, [], 10000, 10).shape[0] == 0
+
+
+def _check_left_balanced(pos, dims):
+    """every node vs all its ancestors: left subtree <= ancestor <= right subtree
+    on the ancestor's split dimension (cukd left-balanced kd-tree invariant)."""
+    n = len(pos)
+    node = np.arange(n)
+    cur = node.copy()
+    while True:
+        parent = (cur + 1) // 2 - 1
+        m = parent >= 0
+        node, cur, parent = node[m], cur[m], parent[m]
+        if len(node) == 0:
+            break
+        left = cur == 2 * parent + 1
+        d = dims[parent]
+        ac = pos[parent, d]
+        ic = pos[node, d]
+        assert np.all(ic[left] <= ac[left]) and np.all(ic[~left] >= ac[~left])
+        cur = parent
+    return True
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 1000, 65537, 300000])
+def test_kdtree_build_left_balanced(n):
+    import pm_amd
+    rng = np.random.default_rng(n)
+    rec = np.zeros((n, 11), np.float32)
+    rec[:, 0:3] = rng.uniform(-20, 20, size=(n, 3))
+    if n > 10:
+        rec[: n // 10, 1] = 0.0        # a plane of ties
+        rec[n // 10: n // 5, 0:3] = 5.0  # exact duplicates
+    rec[:, 6:9] = rng.uniform(0, 1, size=(n, 3))
+    rec[:, 9] = 1.0
+    t = torch.from_numpy(rec.copy()).cuda()
+    b = pm_amd.build_tree(t).cpu().numpy()
+    out = t.cpu().numpy()
+    dims = out[:, 10].view(np.uint32) >> 24
+    assert np.all(dims <= 2)
+    assert np.allclose(b[0], rec[:, :3].min(0)) and np.allclose(b[1], rec[:, :3].max(0))
+    # permutation of the input records (ignoring split_dim byte)
+    key = lambda a: np.lexsort(a[:, :10].view(np.uint32).T[::-1])
+    o2 = out.copy()
+    o2[:, 10] = 0
+    assert np.array_equal(rec[key(rec)][:, :10].view(np.uint32), o2[key(o2)][:, :10].view(np.uint32))
+    _check_left_balanced(out[:, :3], dims.astype(np.int64))
+
+
+def _brute_knn(pts, q, k, r):
+    # same float32 evaluation order as the spec: (dx*dx + dy*dy) + dz*dz
+    diff = (q[:, None, :] - pts[None, :, :]).astype(np.float32)
+    d2 = (diff[..., 0] * diff[..., 0] + diff[..., 1] * diff[..., 1]).astype(np.float32) + diff[..., 2] * diff[..., 2]
+    ids = np.full((len(q), k), -1, np.int32)
+    dd = np.full((len(q), k), np.float32(r * r), np.float32)
+    for i in range(len(q)):
+        ok = np.nonzero(d2[i] < np.float32(r * r))[0]
+        order = ok[np.lexsort((ok, d2[i, ok]))][:k]
+        ids[i, : len(order)] = order
+        dd[i, : len(order)] = d2[i, order]
+    return ids, dd
+
+
+def test_knn_bruteforce_with_ties():
+    import pm_amd
+    rng = np.random.default_rng(7)
+    n = 3000
+    pts = rng.integers(-5, 6, size=(n, 3)).astype(np.float32)   # lattice: many exact ties
+    ph = np.zeros((n, 10), np.float32)
+    ph[:, 0:3] = pts
+    ph[:, 7:10] = 1.0
+    m = pm_amd.PhotonMap(torch.from_numpy(ph).cuda(), 1.0)
+    q = rng.uniform(-6, 6, size=(400, 3)).astype(np.float32)
+    q[:50] = pts[:50]                                           # queries on photons
+    for k, r in [(50, 100.0), (8, 2.5), (64, 1.0), (16, 0.0)]:
+        ids, d2, md = pm_amd.knn(m, torch.from_numpy(q).cuda(), k, r)
+        bi, bd = _brute_knn(pts, q, k, r)
+        assert np.array_equal(ids.cpu().numpy(), bi), (k, r)
+        assert np.array_equal(_bits(d2.cpu().numpy()), _bits(bd)), (k, r)
+        assert np.array_equal(_bits(md.cpu().numpy()), _bits(bd[:, -1]))
+
+
+def test_knn_and_gather_vs_oracle(cornell):
+    import oracle
+    import pm_amd
+    meshes, lights = cornell
+    os_ = oracle.Scene(meshes)
+    g = oracle.trace(os_, lights, 20000, 10, False)
+    c = oracle.trace(os_, lights, 20000, 10, True)
+    gm = pm_amd.PhotonMap(torch.from_numpy(g).cuda(), 1.0, torch.from_numpy(c).cuda(), 0.5)
+    om = oracle.PhotonMap(g, 1.0, c, 0.5)
+    rng = np.random.default_rng(3)
+    q = g[rng.integers(0, len(g), 2000), 0:3] + rng.normal(scale=0.5, size=(2000, 3)).astype(np.float32)
+    q = q.astype(np.float32)
+    ids, d2, md = pm_amd.knn(gm, torch.from_numpy(q).cuda(), 50, 100.0)
+    oi, od, omd = om.knn(q, 50, 100.0)
+    assert np.array_equal(ids.cpu().numpy(), oi)
+    assert np.array_equal(_bits(d2.cpu().numpy()), _bits(od))
+    assert np.array_equal(_bits(md.cpu().numpy()), _bits(omd))
+    brdf = rng.uniform(0, 0.4, size=2000).astype(np.float32)
+    fg = pm_amd.gather_photons(gm, torch.from_numpy(q).cuda(), torch.from_numpy(brdf).cuda()).cpu().numpy()
+    fo = om.gather(q, brdf)
+    assert np.array_equal(_bits(fg), _bits(fo))
+
+
+def test_photon_map_export(cornell):
+    import oracle
+    import pm_amd
+    meshes, lights = cornell
+    g = oracle.trace(oracle.Scene(meshes), lights, 5000, 10, False)
+    m = pm_amd.PhotonMap(torch.from_numpy(g).cuda(), 1.0)
+    e = m.export().cpu().numpy()
+    assert len(e) == len(g)
+    dims = e[:, 10].view(np.uint32) >> 24
+    _check_left_balanced(e[:, :3], dims.astype(np.int64))
+    assert np.all(e[:, 9] == 1.0)
+
+
+def _render_pair(meshes, lights, casted, W, H, spp, tiles=(0, 1)):
+    import oracle
+    import pm_amd
+    os_ = oracle.Scene(meshes)
+    gs = pm_amd.Scene(meshes)
+    gph = pm_amd.run_normal(gs, lights, casted, 10)
+    cph = pm_amd.run_caustics(gs, lights, casted, 10)
+    g_np, c_np = gph.cpu().numpy(), cph.cpu().numpy()
+    gmap, cmap = pm_amd.load_photons(gph, cph)
+    cam = pm_amd.setup_camera((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
+    ocam = oracle.camera_setup((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
+    assert bytes(cam) == bytes(ocam)
+    rgba, rgb = pm_amd.render(gs, cam, W, H, spp, 30, (1, 1, 1), lights, gmap, cmap, tile_rank=tiles[0],
+                              tile_count=tiles[1])
+    om_g = oracle.PhotonMap(g_np, 1.0, c_np, 0.5)
+    om_c = oracle.PhotonMap(c_np, 0.5)
+    orgba, orgb, ost = oracle.render(os_, ocam, W, H, spp, 30, (1, 1, 1), lights, om_g, om_c,
+                                     tile_rank=tiles[0], tile_count=tiles[1])
+    return rgba.cpu().numpy().view(np.uint32), rgb.cpu().numpy(), orgba, orgb, ost
+
+
+@pytest.mark.parametrize("which,casted,W,H,spp", [("cornell", 20000, 64, 48, 2), ("sphere", 20000, 48, 40, 1)])
+def test_render_vs_oracle(which, casted, W, H, spp, request):
+    import pm_amd
+    meshes, lights = request.getfixturevalue(which)
+    rgba, rgb, orgba, orgb, ost = _render_pair(meshes, lights, casted, W, H, spp)
+    st = pm_amd.render_stats()
+    assert (st.pixels, st.path_vertices, st.caustic_queries, st.global_queries, st.rays) == \
+        (ost.pixels, ost.path_vertices, ost.caustic_queries, ost.global_queries, ost.rays)
+    err = np.abs(np.clip(rgb, 0, 1) - np.clip(orgb, 0, 1)).max()
+    assert err <= 1e-3, err
+    exact = np.mean(_bits(rgb) == _bits(orgb))
+    assert exact >= 0.999, exact
+    assert np.mean(rgba != orgba) <= 0.001
+    assert np.all(rgba[0] == 0)   # row 0 is never written (deviceCode.cu:224-229)
+
+
+def test_render_tiles_cover_image(cornell):
+    meshes, lights = cornell
+    parts = []
+    for r in range(3):
+        rgba, rgb, orgba, orgb, _ = _render_pair(meshes, lights, 5000, 40, 36, 1, tiles=(r, 3))
+        assert np.array_equal(_bits(rgb), _bits(orgb)) or np.abs(rgb - orgb).max() <= 1e-3
+        parts.append(rgba)
+    full, _, ofull, _, _ = _render_pair(meshes, lights, 5000, 40, 36, 1)
+    merged = parts[0] | parts[1] | parts[2]
+    assert np.array_equal(merged, full)
+
+
+def test_render_empty_maps(cornell):
+    import pm_amd
+    meshes, lights = cornell
+    gs = pm_amd.Scene(meshes)
+    empty = torch.zeros((0, 10), dtype=torch.float32, device="cuda")
+    gmap, cmap = pm_amd.load_photons(empty, empty)
+    cam = pm_amd.setup_camera((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, 32, 32)
+    rgba, rgb = pm_amd.render(gs, cam, 32, 32, 1, 30, (1, 1, 1), lights, gmap, cmap)
+    assert torch.isfinite(rgb).all()
