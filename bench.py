@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""bench.py — photon-mapping hot path on MI355X (BASELINE.json metric).
+
+One step = one full frame of the reference pipeline on synthetic input:
+  trace    runNormal + runCaustics (photon-mapping/src/hostCode.cu:112-138)
+  exchange all-gather of the photon buffers over RCCL (N > 1 only)
+  build    loadPhotons: global + caustic kd-trees (ray-tracer/src/hostCode.cu:54-99)
+  render   owlRayGenLaunch2D(simpleRayGen) final gather (ray-tracer/src/hostCode.cu:231-237)
+Workload (BASELINE config 3): Sponza-class procedural scene (pm_amd.scenes,
+~267k triangles, 373 meshes; Sponza itself is not available offline),
+10M diffuse + 1M caustic photons per GPU, 1920x1080, spp 1, depth 30,
+k = 50, max_depth 10. value = emitted photons of the whole job / wall time of
+a step (Mphotons/s traced + gathered). N > 1: photon-index sharding with a
+single all-gather, replicated kd-tree build, 16x16-tile-sharded final gather,
+image reduce to rank 0 ("weak": photons per GPU fixed, config 4 at N = 8).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "photon-mapping_amd"), os.path.join(ROOT, "oracle")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CAMERA = dict(look_from=(80.0, 30.0, 0.0), look_at=(10.0, 20.0, 0.0), look_up=(0.0, 1.0, 0.0), fovy=0.87)
+SKY = (1.0, 1.0, 1.0)
+
+
+def knn_query_bytes(n_photons: int, k: int = 50) -> int:
+    """Algorithmic bytes of one kNN radiance query: 16*ceil(log2 N) + 28*k + 24."""
+    return 16 * math.ceil(math.log2(max(2, n_photons))) + 28 * k + 24
+
+
+def allgather_rows(t, world, dist, torch):
+    """All-gather a (n_r, 10) float32 tensor of variable length; rank-order concat."""
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    m = max(ns)
+    pad = torch.zeros((max(m, 1), t.shape[1]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    out = torch.empty((world * max(m, 1), t.shape[1]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, pad)
+    return torch.cat([out[r * max(m, 1): r * max(m, 1) + ns[r]] for r in range(world)])
+
+
+def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
+    """Scalar oracle (oracle/libpm_oracle.so, pthreads) on a bounded sample of the
+    same workload, scaled linearly to one frame."""
+    import numpy as np
+    import oracle
+    t0 = time.time()
+    sc = oracle.Scene(meshes)
+    counts_g = oracle.photons_per_light(lights, args.casted)
+    counts_c = oracle.photons_per_light(lights, args.caustic)
+    P = sum(counts_g) + sum(counts_c)
+    frac = args.cpu_sample_photons / max(1, sum(counts_g))
+    sg = int(sum(counts_g) * frac)
+    scn = int(sum(counts_c) * frac)
+    t = time.time()
+    g = oracle.trace(sc, lights, args.casted, args.max_depth, False, nthreads=nthreads, g_range=(0, sg))
+    c = oracle.trace(sc, lights, args.caustic, args.max_depth, True, nthreads=nthreads, g_range=(0, scn))
+    t_trace = (time.time() - t) / frac
+    t = time.time()
+    gm = oracle.PhotonMap(g, 1.0, c, 0.5)
+    cm = oracle.PhotonMap(c, 0.5)
+    t_build_s = time.time() - t
+    n_s = max(2, len(g) + len(c))
+    t_build = t_build_s * (n_global_full / n_s) * (math.log2(max(2, n_global_full)) / math.log2(n_s))
+    cam = oracle.camera_setup(CAMERA["look_from"], CAMERA["look_at"], CAMERA["look_up"], CAMERA["fovy"],
+                              args.width, args.height)
+    rows = args.cpu_sample_rows
+    r0 = args.height // 2 - rows // 2
+    t = time.time()
+    oracle.render(sc, cam, args.width, args.height, args.spp, args.depth, SKY, lights, gm, cm,
+                  rows=(r0, r0 + rows), nthreads=nthreads)
+    t_render = (time.time() - t) * args.height / rows
+    total = t_trace + t_build + t_render
+    return {
+        "value": P / total / 1e6, "unit": "Mphotons/s", "cores": nthreads, "kind": "port",
+        "sample": (f"oracle (pthreads x{nthreads}) traced {sg + scn} of {P} photons (scaled x{1 / frac:.1f}), "
+                   f"kd-built {n_s} photons (scaled N log N to {n_global_full}), rendered {rows} of "
+                   f"{args.height} rows at {args.width} px (scaled x{args.height / rows:.1f}) with the sampled "
+                   f"maps; wall {time.time() - t0:.1f}s"),
+        "ms_per_frame": total * 1e3,
+        "phase_s": {"trace": t_trace, "build": t_build, "render": t_render},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--casted", type=int, default=10_000_000, help="diffuse photons per GPU")
+    ap.add_argument("--caustic", type=int, default=1_000_000, help="caustic photons per GPU")
+    ap.add_argument("--max-depth", type=int, default=10)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1)
+    ap.add_argument("--depth", type=int, default=30)
+    ap.add_argument("--scene", default="sponza", choices=["sponza", "cornell"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample-photons", type=int, default=200_000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=8)
+    args = ap.parse_args()
+
+    import torch
+    import pm_amd
+    from pm_amd import scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus or (world == 1 and args.gpus == 1), f"--gpus {args.gpus} but WORLD_SIZE={world}"
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    if args.scene == "sponza":
+        obj = os.environ.get("PM_SPONZA_OBJ")
+        if obj and os.path.exists(obj):
+            meshes, lights = pm_amd.load_scene_file(obj)
+            scene_name = f"sponza.obj ({obj})"
+        else:
+            meshes, lights = scenes.sponza_class()
+            scene_name = "sponza-class procedural (pm_amd.scenes)"
+    else:
+        meshes, lights = pm_amd.load_scene_file(os.path.join(ROOT, "tests", "golden", "scenes", "cornell-box",
+                                                             "cornell-box.glb"))
+        scene_name = "cornell-box.glb"
+    ntri = sum(len(m.indices) for m in meshes)
+    casted_total = args.casted * world       # weak scaling: photons per GPU fixed
+    caustic_total = args.caustic * world
+    scene = pm_amd.Scene(meshes)
+    cam = pm_amd.setup_camera(CAMERA["look_from"], CAMERA["look_at"], CAMERA["look_up"], CAMERA["fovy"],
+                              args.width, args.height)
+    emitted = sum(pm_amd.compute_photons_per_watt(lights, casted_total)) + \
+        sum(pm_amd.compute_photons_per_watt(lights, caustic_total))
+    cap_g = pm_amd.trace_capacity(lights, casted_total, args.max_depth, False, rank, world)
+    cap_c = pm_amd.trace_capacity(lights, caustic_total, args.max_depth, True, rank, world)
+    gbuf = torch.empty((max(1, cap_g), 10), dtype=torch.float32, device="cuda")
+    cbuf = torch.empty((max(1, cap_c), 10), dtype=torch.float32, device="cuda")
+    rgba = torch.zeros((args.height, args.width), dtype=torch.int32, device="cuda")
+    info = {}
+
+    def step():
+        g = pm_amd.run_normal(scene, lights, casted_total, args.max_depth, shard_rank=rank, shard_count=world,
+                              out=gbuf)
+        t_tr = pm_amd.phase_us("trace") + pm_amd.phase_us("compact")
+        c = pm_amd.run_caustics(scene, lights, caustic_total, args.max_depth, shard_rank=rank, shard_count=world,
+                                out=cbuf)
+        t_tr += pm_amd.phase_us("trace") + pm_amd.phase_us("compact")
+        te = time.time()
+        if world > 1:
+            g = allgather_rows(g, world, dist, torch)
+            c = allgather_rows(c, world, dist, torch)
+            torch.cuda.synchronize()
+        t_ex = (time.time() - te) * 1e6
+        gmap = pm_amd.PhotonMap(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER)
+        t_kd = pm_amd.phase_us("kdbuild")
+        cmap = pm_amd.PhotonMap(c, pm_amd.CAUSTICS_PHOTON_POWER)
+        t_kd += pm_amd.phase_us("kdbuild")
+        pm_amd.render(scene, cam, args.width, args.height, args.spp, args.depth, SKY, lights, gmap, cmap,
+                      tile_rank=rank, tile_count=world, want_rgb=False, rgba=rgba)
+        st = pm_amd.render_stats()
+        if world > 1:
+            dist.reduce(rgba, dst=0, op=dist.ReduceOp.SUM)
+        info.update(n_global=int(gmap.n), n_caustic=int(cmap.n), stats=st,
+                    us={"trace": t_tr, "exchange": t_ex, "kdbuild": t_kd, "paths": pm_amd.phase_us("paths"),
+                        "gather": pm_amd.phase_us("gather"), "gather_global": pm_amd.phase_us("gather_global"),
+                        "resolve": pm_amd.phase_us("resolve")})
+        del gmap, cmap
+
+    for _ in range(args.warmup):
+        step()
+        rgba.zero_()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gather_us = []
+    for _ in range(args.steps):
+        step()
+        gather_us.append(info["us"]["gather_global"])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = emitted * args.steps / elapsed / 1e6
+    st = info["stats"]
+    us = info["us"]
+    nq_g = int(st.global_queries)
+    t_g = sum(gather_us) / len(gather_us) * 1e-6
+    bpq = knn_query_bytes(info["n_global"], 50)
+    achieved = bpq * nq_g / t_g / 1e9 if t_g > 0 else 0.0
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_gather_global.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            if pmc.get("workload") == [args.scene, args.casted, args.caustic, args.width, args.height, args.spp]:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    queries = int(st.global_queries + st.caustic_queries)
+    out = {
+        "metric": "Mphotons/s traced + kNN gathers/s; ms/frame Sponza 10M photons",
+        "value": round(value, 4),
+        "unit": "Mphotons/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (procedural Sponza-class scene; photons from the reference's own emission model)",
+        "config": {"workload": f"config3: {scene_name}, {casted_total} diffuse + {caustic_total} caustic photons, "
+                               f"{args.width}x{args.height} spp {args.spp}, depth {args.depth}, k 50",
+                   "triangles": ntri, "parallelism": f"photon-shard{world}+tile{world}" if world > 1 else "1 GPU"},
+        "ms_per_frame": round(ms_per_step, 3),
+        "mphotons_traced_per_s": round(emitted / (us["trace"] * 1e-6) / 1e6, 3) if us["trace"] else None,
+        "knn_gathers_per_s": round(queries / (us["gather"] * 1e-6), 1) if us["gather"] else None,
+        "phases_ms": {k: round(v / 1e3, 3) for k, v in us.items()},
+        "photon_maps": {"global": info["n_global"], "caustic": info["n_caustic"]},
+        "render": {"path_vertices": int(st.path_vertices), "caustic_queries": int(st.caustic_queries),
+                   "global_queries": nq_g, "rays": int(st.rays)},
+        "roofline": {"bound": "hbm", "kernel": "pmd::k_gather<1> (global-map kNN radiance estimate)",
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "bytes_per_query": bpq, "queries_per_launch": nq_g,
+                     "avg_launch_ms": round(t_g * 1e3, 3)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(meshes, lights, args, info["n_global"], args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -113,7 +113,8 @@ const char* pm_status_string(int status);
 int pm_device_count(int32_t* count);
 /* Microseconds of the last kernel(s) of a phase, measured with hipEvents on
  * the stream the kernels ran on. phase: 0 trace, 1 compaction, 2 kd-build,
- * 3 render-paths, 4 knn-gather, 5 resolve, 6 bvh-build. */
+ * 3 render-paths, 4 knn-gather (all), 5 resolve, 6 bvh-build, 7 the global-map
+ * gather launch alone (the dominant kernel). */
 int pm_last_phase_us(int32_t phase, double* us);
 
 /* ---- scene (world.cpp:3-58 loadGeometry; OptiX GAS+IAS -> HIP LBVH) ------- */

@@ -467,6 +467,7 @@ int pm_render(pm_scene* sc, const pm_render_params* P, const pm_light* lights, i
   reset_phase(PH_PATHS);
   reset_phase(PH_GATHER);
   reset_phase(PH_RESOLVE);
+  reset_phase(PH_GATHER_GLOBAL);
   pm_render_stats stats{};
   PM_TRY_ST(render_impl(sc, P, lights, nl, gmap, cmap, rgba, rgb, &stats, s));
   PM_TRY_ST(hipStreamSynchronize(s));

@@ -109,6 +109,7 @@ __device__ __forceinline__ v3 gather_one(const float4* __restrict__ nodes, const
   return divf(flux, (1 - (2.f / 3.f) * (1.f / kConeFilterC)) * 2 * kPI * r2);
 }
 
+template <int TAG>
 __global__ __launch_bounds__(256) void k_gather(const float4* nodes, const float4* payload, int n,
                                                 const float4* qb, int64_t nq, float4* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -150,9 +151,13 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s) {
+hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,
+                         int tag) {
   if (nq <= 0) return hipSuccess;
-  k_gather<<<grid_for(nq, 256), 256, 0, s>>>(m->nodes.p, m->payload.p, (int)m->n, qb, nq, out);
+  if (tag == 1)
+    k_gather<1><<<grid_for(nq, 256), 256, 0, s>>>(m->nodes.p, m->payload.p, (int)m->n, qb, nq, out);
+  else
+    k_gather<0><<<grid_for(nq, 256), 256, 0, s>>>(m->nodes.p, m->payload.p, (int)m->n, qb, nq, out);
   return hipGetLastError();
 }
 

@@ -42,7 +42,7 @@ namespace pmd {
 
 // phase timers (pm_last_phase_us)
 enum Phase { PH_TRACE = 0, PH_COMPACT = 1, PH_KDBUILD = 2, PH_PATHS = 3, PH_GATHER = 4, PH_RESOLVE = 5, PH_BVH = 6,
-             PH_COUNT = 7 };
+             PH_GATHER_GLOBAL = 7, PH_COUNT = 8 };
 struct PhaseTimer {
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t s = nullptr;
@@ -59,7 +59,8 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& tri_host, hipStre
 hipError_t kd_build(const float4* d_elems, int64_t n, float4* d_nodes, hipStream_t s);
 
 // K = 50 gather (gatherPhotons) for a batch of queries.
+// tag 0: API / caustic-map launches, 1: global-map launch (separate kernel symbol for rocprof)
 hipError_t launch_gather(const pm_photon_map* m, const float4* d_query /*pos, brdf*/, int64_t nq,
-                         float4* d_out, hipStream_t s);
+                         float4* d_out, hipStream_t s, int tag = 0);
 
 }  // namespace pmd

@@ -414,8 +414,9 @@ hipError_t render_impl(pm_scene* sc, const pm_render_params* P, const pm_light* 
       k_compact_q<<<grid_for(NG, 256), 256, 0, s>>>(gq.p, gvalid.p, gidx.p, NG, gdense.p);
       PM_HIP_TRY(hipGetLastError());
     }
-    PM_HIP_TRY(launch_gather(cmap, cdense.p, NC, cres.p, s));
-    PM_HIP_TRY(launch_gather(gmap, gdense.p, NGv, gres.p, s));
+    PM_HIP_TRY(launch_gather(cmap, cdense.p, NC, cres.p, s, 0));
+    PhaseTimer tg(PH_GATHER_GLOBAL, s);
+    PM_HIP_TRY(launch_gather(gmap, gdense.p, NGv, gres.p, s, 1));
   }
   {
     PhaseTimer tm(PH_RESOLVE, s);

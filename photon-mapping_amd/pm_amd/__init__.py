@@ -31,7 +31,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PM_HIP_LIB", os.path.join(_HERE, "..", "lib", "libpm_hip.so"))
 
 PM_OK, PM_ERR_INVALID, PM_ERR_HIP, PM_ERR_OOM, PM_ERR_NO_DEVICE, PM_ERR_IO, PM_ERR_CAPACITY, PM_ERR_OVERFLOW = range(8)
-PHASES = {"trace": 0, "compact": 1, "kdbuild": 2, "paths": 3, "gather": 4, "resolve": 5, "bvh": 6}
+PHASES = {"trace": 0, "compact": 1, "kdbuild": 2, "paths": 3, "gather": 4, "resolve": 5, "bvh": 6,
+          "gather_global": 7}
 
 
 class PMError(RuntimeError):
