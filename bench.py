@@ -36,20 +36,6 @@ def knn_query_bytes(n_photons: int, k: int = 50) -> int:
     return 16 * math.ceil(math.log2(max(2, n_photons))) + 28 * k + 24
 
 
-def allgather_rows(t, world, dist, torch):
-    """All-gather a (n_r, 10) float32 tensor of variable length; rank-order concat."""
-    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
-    ns = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(ns, n)
-    ns = [int(x.item()) for x in ns]
-    m = max(ns)
-    pad = torch.zeros((max(m, 1), t.shape[1]), dtype=t.dtype, device=t.device)
-    pad[: t.shape[0]] = t
-    out = torch.empty((world * max(m, 1), t.shape[1]), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, pad)
-    return torch.cat([out[r * max(m, 1): r * max(m, 1) + ns[r]] for r in range(world)])
-
-
 def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
     """Scalar oracle (oracle/libpm_oracle.so, pthreads) on a bounded sample of the
     same workload, scaled linearly to one frame."""
@@ -114,6 +100,7 @@ def main():
 
     import torch
     import pm_amd
+    from pm_amd import dist as pmdist
     from pm_amd import scenes
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,8 +129,6 @@ def main():
     casted_total = args.casted * world       # weak scaling: photons per GPU fixed
     caustic_total = args.caustic * world
     scene = pm_amd.Scene(meshes)
-    cam = pm_amd.setup_camera(CAMERA["look_from"], CAMERA["look_at"], CAMERA["look_up"], CAMERA["fovy"],
-                              args.width, args.height)
     emitted = sum(pm_amd.compute_photons_per_watt(lights, casted_total)) + \
         sum(pm_amd.compute_photons_per_watt(lights, caustic_total))
     cap_g = pm_amd.trace_capacity(lights, casted_total, args.max_depth, False, rank, world)
@@ -152,34 +137,14 @@ def main():
     cbuf = torch.empty((max(1, cap_c), 10), dtype=torch.float32, device="cuda")
     rgba = torch.zeros((args.height, args.width), dtype=torch.int32, device="cuda")
     info = {}
+    cfg = pmdist.FrameConfig(casted=casted_total, caustic=caustic_total, max_depth=args.max_depth,
+                             width=args.width, height=args.height, spp=args.spp, depth=args.depth, sky=SKY,
+                             camera=CAMERA)
+    backend = pmdist.GpuBackend(scene, lights, cfg, rank, world, gbuf=gbuf, cbuf=cbuf)
 
     def step():
-        g = pm_amd.run_normal(scene, lights, casted_total, args.max_depth, shard_rank=rank, shard_count=world,
-                              out=gbuf)
-        t_tr = pm_amd.phase_us("trace") + pm_amd.phase_us("compact")
-        c = pm_amd.run_caustics(scene, lights, caustic_total, args.max_depth, shard_rank=rank, shard_count=world,
-                                out=cbuf)
-        t_tr += pm_amd.phase_us("trace") + pm_amd.phase_us("compact")
-        te = time.time()
-        if world > 1:
-            g = allgather_rows(g, world, dist, torch)
-            c = allgather_rows(c, world, dist, torch)
-            torch.cuda.synchronize()
-        t_ex = (time.time() - te) * 1e6
-        gmap = pm_amd.PhotonMap(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER)
-        t_kd = pm_amd.phase_us("kdbuild")
-        cmap = pm_amd.PhotonMap(c, pm_amd.CAUSTICS_PHOTON_POWER)
-        t_kd += pm_amd.phase_us("kdbuild")
-        pm_amd.render(scene, cam, args.width, args.height, args.spp, args.depth, SKY, lights, gmap, cmap,
-                      tile_rank=rank, tile_count=world, want_rgb=False, rgba=rgba)
-        st = pm_amd.render_stats()
-        if world > 1:
-            dist.reduce(rgba, dst=0, op=dist.ReduceOp.SUM)
-        info.update(n_global=int(gmap.n), n_caustic=int(cmap.n), stats=st,
-                    us={"trace": t_tr, "exchange": t_ex, "kdbuild": t_kd, "paths": pm_amd.phase_us("paths"),
-                        "gather": pm_amd.phase_us("gather"), "gather_global": pm_amd.phase_us("gather_global"),
-                        "resolve": pm_amd.phase_us("resolve")})
-        del gmap, cmap
+        _, fi = pmdist.frame(backend, rank, world, dist, rgba)
+        info.update(n_global=fi["n_global"], n_caustic=fi["n_caustic"], stats=pm_amd.render_stats(), us=fi["us"])
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,120 @@
+"""Multi-GPU frame driver: one process per GPU, torch.distributed
+over RCCL ("nccl" backend) on MI355X, gloo on CPU for tests.
+
+  1. trace      rank r traces global photon indices [r*P/G, (r+1)*P/G) of every
+                mode; seeds are the per-light launch ids, so the union is
+                bit-identical to the 1-GPU trace (pm_trace_params.shard_*).
+  2. exchange   ONE all-gather per photon buffer (counts first, then the padded
+                buffers); rank-order concatenation reproduces the 1-GPU array.
+  3. build      every rank builds the same kd-trees (replicated; cheaper than a
+                second exchange).
+  4. render     16x16 image tiles dealt round robin (tile % G == r).
+  5. assemble   tiles are disjoint, so an integer SUM-reduce to rank 0 merges
+                the RGBA8 image exactly.
+The compute backend is pluggable: `GpuBackend` (libpm_hip.so) in production;
+tests plug the CPU oracle in to check the orchestration with gloo.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+
+@dataclass
+class FrameConfig:
+    casted: int
+    caustic: int
+    max_depth: int = 10
+    width: int = 64
+    height: int = 48
+    spp: int = 1
+    depth: int = 30
+    sky: tuple = (1.0, 1.0, 1.0)
+    camera: dict = field(default_factory=lambda: dict(look_from=(80.0, 30.0, 0.0), look_at=(10.0, 20.0, 0.0),
+                                                       look_up=(0.0, 1.0, 0.0), fovy=0.87))
+
+
+def shard_range(total: int, rank: int, world: int):
+    return total * rank // world, total * (rank + 1) // world
+
+
+def allgather_rows(t, world: int, dist):
+    """Variable-length all-gather of an (n_r, C) tensor, concatenated in rank order."""
+    import torch
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    m = max(1, max(ns))
+    pad = torch.zeros((m, t.shape[1]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    if t.device.type == "cuda":
+        out = torch.empty((world * m, t.shape[1]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, pad)
+        parts = [out[r * m: r * m + ns[r]] for r in range(world)]
+    else:
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(bufs, pad)
+        parts = [bufs[r][: ns[r]] for r in range(world)]
+    return torch.cat(parts)
+
+
+class GpuBackend:
+    """libpm_hip.so through pm_amd (device tensors on the current cuda device)."""
+
+    def __init__(self, scene, lights, cfg: FrameConfig, rank: int, world: int, gbuf=None, cbuf=None):
+        import pm_amd
+        self.pm = pm_amd
+        self.scene, self.lights, self.cfg = scene, lights, cfg
+        self.gbuf, self.cbuf = gbuf, cbuf
+        self.cam = pm_amd.setup_camera(cfg.camera["look_from"], cfg.camera["look_at"], cfg.camera["look_up"],
+                                       cfg.camera["fovy"], cfg.width, cfg.height)
+        self.phase = {}
+
+    def trace(self, caustics: bool, rank: int, world: int):
+        pm = self.pm
+        casted = self.cfg.caustic if caustics else self.cfg.casted
+        out = self.cbuf if caustics else self.gbuf
+        t = pm.run_point_light_ray_gen(self.scene, self.lights, casted, self.cfg.max_depth, caustics,
+                                       shard_rank=rank, shard_count=world, out=out)
+        self.phase["trace"] = self.phase.get("trace", 0.0) + pm.phase_us("trace") + pm.phase_us("compact")
+        return t
+
+    def maps(self, g, c):
+        pm = self.pm
+        gm = pm.PhotonMap(g, pm.PHOTON_POWER, c, pm.CAUSTICS_PHOTON_POWER)
+        kd = pm.phase_us("kdbuild")
+        cm = pm.PhotonMap(c, pm.CAUSTICS_PHOTON_POWER)
+        self.phase["kdbuild"] = kd + pm.phase_us("kdbuild")
+        return gm, cm
+
+    def render(self, gm, cm, tile_rank: int, tile_count: int, rgba):
+        pm = self.pm
+        c = self.cfg
+        pm.render(self.scene, self.cam, c.width, c.height, c.spp, c.depth, c.sky, self.lights, gm, cm,
+                  tile_rank=tile_rank, tile_count=tile_count, want_rgb=False, rgba=rgba)
+        for k in ("paths", "gather", "gather_global", "resolve"):
+            self.phase[k] = pm.phase_us(k)
+        return rgba
+
+
+def frame(backend, rank: int, world: int, dist=None, rgba=None):
+    """One frame through `backend`; returns (rgba on rank 0 (merged), info)."""
+    import torch
+    backend.phase = {}
+    g = backend.trace(False, rank, world)
+    c = backend.trace(True, rank, world)
+    te = time.time()
+    if world > 1:
+        g = allgather_rows(g, world, dist)
+        c = allgather_rows(c, world, dist)
+        if g.device.type == "cuda":
+            torch.cuda.synchronize()
+    backend.phase["exchange"] = (time.time() - te) * 1e6
+    gm, cm = backend.maps(g, c)
+    rgba = backend.render(gm, cm, rank, world, rgba)
+    if world > 1:
+        dist.reduce(rgba, dst=0, op=dist.ReduceOp.SUM)
+    info = {"n_global": int(gm.n), "n_caustic": int(cm.n), "n_global_rows": int(g.shape[0]),
+            "us": dict(backend.phase)}
+    return rgba, info

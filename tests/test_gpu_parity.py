@@ -170,9 +170,9 @@ def _brute_knn(pts, q, k, r):
     diff = (q[:, None, :] - pts[None, :, :]).astype(np.float32)
     d2 = (diff[..., 0] * diff[..., 0] + diff[..., 1] * diff[..., 1]).astype(np.float32) + diff[..., 2] * diff[..., 2]
     ids = np.full((len(q), k), -1, np.int32)
-    dd = np.full((len(q), k), np.float32(r * r), np.float32)
+    dd = np.full((len(q), k), (np.float32(r) * np.float32(r)), np.float32)
     for i in range(len(q)):
-        ok = np.nonzero(d2[i] < np.float32(r * r))[0]
+        ok = np.nonzero(d2[i] < (np.float32(r) * np.float32(r)))[0]
         order = ok[np.lexsort((ok, d2[i, ok]))][:k]
         ids[i, : len(order)] = order
         dd[i, : len(order)] = d2[i, order]
