@@ -249,11 +249,11 @@ __device__ __forceinline__ bool wt_hit(const float4 a, const float4 b, const flo
 
 // slab test for one box given as (x0,x1,y0,y1,z0,z1)
 __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, float z0, float z1, const Ray& r,
-                                     float tmin, float tmax) {
+                                     float tmin, float tmax, float& tn) {
   const float t0x = (x0 - r.o.x) * r.inv.x, t1x = (x1 - r.o.x) * r.inv.x;
   const float t0y = (y0 - r.o.y) * r.inv.y, t1y = (y1 - r.o.y) * r.inv.y;
   const float t0z = (z0 - r.o.z) * r.inv.z, t1z = (z1 - r.o.z) * r.inv.z;
-  const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+  tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
   const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
   return tn <= tf;
 }
@@ -281,10 +281,19 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
     const float4 n2 = S.nodes[4 * node + 2];
     const int4 n3 = *reinterpret_cast<const int4*>(&S.nodes[4 * node + 3]);
     const float lim = (ANY || h.slot < 0) ? tmax * 1.00001f : h.t * 1.00001f;
-    const bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, tmin, lim);
-    const bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, tmin, lim);
+    float tnl, tnr;
+    const bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, tmin, lim, tnl);
+    const bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, tmin, lim, tnr);
     int next = -1;
+    // near child first: visit order only changes speed (closest hit is the
+    // argmin over (t, id) regardless of order)
+    const bool swap = !ANY && hl && hr && tnr < tnl;
     int cand[2] = {hl ? n3.x : INT32_MAX, hr ? n3.y : INT32_MAX};
+    if (swap) {
+      const int t = cand[0];
+      cand[0] = cand[1];
+      cand[1] = t;
+    }
 #pragma unroll
     for (int c = 0; c < 2; c++) {
       const int ch = cand[c];

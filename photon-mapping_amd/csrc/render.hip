@@ -277,6 +277,60 @@ __global__ void k_compact_q(const float4* q, const uint32_t* valid, const uint32
   if (valid[i]) dense[idx[i]] = q[i];
 }
 
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+
+// 30-bit Morton code of each query position (scene bounds) + identity permutation
+__global__ void k_query_morton(const float4* q, int64_t n, float3 lo, float3 inv, uint32_t* keys, uint32_t* perm) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = q[i];
+  const float fx = fminf(fmaxf((p.x - lo.x) * inv.x * 1024.0f, 0.0f), 1023.0f);
+  const float fy = fminf(fmaxf((p.y - lo.y) * inv.y * 1024.0f, 0.0f), 1023.0f);
+  const float fz = fminf(fmaxf((p.z - lo.z) * inv.z * 1024.0f, 0.0f), 1023.0f);
+  keys[i] = (spread3((uint32_t)fx) << 2) | (spread3((uint32_t)fy) << 1) | spread3((uint32_t)fz);
+  perm[i] = (uint32_t)i;
+}
+__global__ void k_permute_q(const float4* src, const uint32_t* perm, int64_t n, float4* dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dst[i] = src[perm[i]];
+}
+__global__ void k_unpermute_q(const float4* src, const uint32_t* perm, int64_t n, float4* dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dst[perm[i]] = src[i];
+}
+
+// Gather in Morton order of the query points (a pure permutation: results are
+// bitwise unchanged) so the lanes of a wave walk the same kd-tree nodes.
+static hipError_t sorted_gather(const pm_photon_map* m, const float4* dense, int64_t n, float4* res,
+                                const pm_box& bb, int tag, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  DevBuf<uint32_t> keys(n), perm(n);
+  DevBuf<float4> qs(n), rs(n);
+  if (!keys.p || !perm.p || !qs.p || !rs.p) return hipErrorOutOfMemory;
+  const float3 lo = make_float3(bb.lower.x, bb.lower.y, bb.lower.z);
+  const float ex = bb.upper.x - bb.lower.x, ey = bb.upper.y - bb.lower.y, ez = bb.upper.z - bb.lower.z;
+  const float3 inv = make_float3(ex > 0.f ? 1.0f / ex : 0.f, ey > 0.f ? 1.0f / ey : 0.f, ez > 0.f ? 1.0f / ez : 0.f);
+  k_query_morton<<<grid_for(n, 256), 256, 0, s>>>(dense, n, lo, inv, keys.p, perm.p);
+  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(radix_sort_pairs(keys.p, perm.p, n, 30, s));
+  k_permute_q<<<grid_for(n, 256), 256, 0, s>>>(dense, perm.p, n, qs.p);
+  PM_HIP_TRY(hipGetLastError());
+  {
+    PhaseTimer tg(tag == 1 ? PH_GATHER_GLOBAL : PH_COUNT, s);
+    PM_HIP_TRY(launch_gather(m, qs.p, n, rs.p, s, tag));
+  }
+  k_unpermute_q<<<grid_for(n, 256), 256, 0, s>>>(rs.p, perm.p, n, res);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, const uint32_t* voff, const uint32_t* cnt,
                                                  PathOut O, const uint32_t* cidx, const float4* cres,
                                                  const uint32_t* gidx, const float4* gres, uint32_t* rgba,
@@ -414,9 +468,8 @@ hipError_t render_impl(pm_scene* sc, const pm_render_params* P, const pm_light* 
       k_compact_q<<<grid_for(NG, 256), 256, 0, s>>>(gq.p, gvalid.p, gidx.p, NG, gdense.p);
       PM_HIP_TRY(hipGetLastError());
     }
-    PM_HIP_TRY(launch_gather(cmap, cdense.p, NC, cres.p, s, 0));
-    PhaseTimer tg(PH_GATHER_GLOBAL, s);
-    PM_HIP_TRY(launch_gather(gmap, gdense.p, NGv, gres.p, s, 1));
+    PM_HIP_TRY(sorted_gather(cmap, cdense.p, NC, cres.p, sc->bounds, 0, s));
+    PM_HIP_TRY(sorted_gather(gmap, gdense.p, NGv, gres.p, sc->bounds, 1, s));
   }
   {
     PhaseTimer tm(PH_RESOLVE, s);
