@@ -13,6 +13,9 @@
 // stably partitioned around it with one fused flag pass, one u64 scan and one
 // scatter. Subtree ranges are identical in the three lists, so a single tag
 // array tracks subtree membership. Ties are broken by the original index.
+#include <algorithm>
+#include <cstdlib>
+
 #include "pm_internal.hpp"
 
 namespace pmd {
@@ -213,6 +216,45 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
       nxt[d] = t;
     }
   }
+  return hipSuccess;
+}
+
+// ---------------------------------------------------------------- buckets
+__global__ void k_kd_buckets(const float4* nodes, int64_t n, int first, int nb, int levels, float4* out) {
+  const int slots = (1 << levels) - 1;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)nb * slots) return;
+  const int64_t b = i / slots;
+  const int sl = (int)(i % slots);
+  const int lvl = 31 - __clz(sl + 1);            // level inside the subtree
+  const int j = sl + 1 - (1 << lvl);             // position in that level
+  const int64_t root = first + b;
+  const int64_t t = ((root + 1) << lvl) - 1 + j;  // implicit index of the node
+  out[i] = t < n ? nodes[t] : make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(-1));
+}
+
+hipError_t kd_make_buckets(pm_photon_map* m, hipStream_t s) {
+  const int64_t n = m->n;
+  m->bucket_first = INT32_MAX;
+  m->bucket_slots = 0;
+  m->bucket_data.reset();
+  int B = kBucketLevels;
+  if (const char* e = std::getenv("PM_KD_BUCKET_LEVELS")) B = std::atoi(e);   // tuning knob; 0 = off
+  if (n <= 0 || B <= 0) return hipSuccess;
+  int H = 0;
+  while ((1ll << H) <= n) H++;                   // levels
+  const int lb = H > B ? H - B : 0;
+  const int levels = H - lb;
+  const int first = (1 << lb) - 1;
+  const int nb = (int)std::min<int64_t>(1ll << lb, std::max<int64_t>(0, n - first));
+  const int slots = (1 << levels) - 1;
+  m->bucket_data.alloc((size_t)nb * slots);
+  if (!m->bucket_data.p) return hipErrorOutOfMemory;
+  k_kd_buckets<<<grid_for((int64_t)nb * slots, 256), 256, 0, s>>>(m->nodes.p, n, first, nb, levels,
+                                                                 m->bucket_data.p);
+  PM_HIP_TRY(hipGetLastError());
+  m->bucket_first = first;
+  m->bucket_slots = slots;
   return hipSuccess;
 }
 

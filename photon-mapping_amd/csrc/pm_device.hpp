@@ -260,6 +260,15 @@ __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, flo
 
 constexpr int kStackDepth = 64;
 
+// Bottom levels of a left-balanced kd-tree stored subtree-contiguously: node t
+// >= first is a bucket root whose subtree (level order, `slots` = 2^B - 1
+// entries, missing nodes = +inf sentinels) lives at data[(t - first) * slots].
+struct KdBuckets {
+  const float4* data;
+  int32_t first;     // INT32_MAX: no buckets
+  int32_t slots;
+};
+
 struct HitInfo {
   float t;
   int32_t slot;   // triangle slot (leaf order) or -1

@@ -21,26 +21,42 @@ struct LightDev {
   float4 rgb;   // xyz
 };
 
+// Each lane traces several photons back to back (i, i + stride, ...): when a
+// photon's path ends the lane immediately starts its next photon, so a wave
+// is not held by its longest path (path lengths range over 1..max_depth).
+constexpr int kPhotonsPerLane = 8;
+
 __global__ __launch_bounds__(kTBlock) void k_trace_photons(DevScene S, const LightDev* lights, const int64_t* loff,
                                                            int nl, int64_t g_lo, int64_t np, int maxd,
                                                            int caustic, pm_photon* slots, uint32_t* cnt,
                                                            int* overflow) {
   __shared__ int stack[kStackDepth * kTBlock];
-  const int64_t i = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
-  if (i >= np) return;
-  const int64_t g = g_lo + i;
-  int l = 0;
-  while (l < nl - 1 && g >= loff[l + 1]) l++;
-  const uint32_t id = (uint32_t)(g - loff[l]);
-  const LightDev L = lights[l];
-  uint32_t rng = lcg_init(id, 0u);
-  v3 color = {L.rgb.x, L.rgb.y, L.rgb.z};
-  v3 o = {L.pos.x, L.pos.y, L.pos.z};
-  v3 d = random_point_in_unit_sphere(rng);
-  const float tmin = kEPS;
-  uint32_t n = 0;
+  const int64_t stride = (int64_t)gridDim.x * kTBlock;
+  int64_t i = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
   int* st = stack + threadIdx.x;
-  for (int b = 0; b < maxd; b++) {
+  const float tmin = kEPS;
+  bool alive = false;
+  uint32_t rng = 0, n = 0;
+  int b = 0;
+  v3 color = {0.f, 0.f, 0.f}, o = {0.f, 0.f, 0.f}, d = {0.f, 0.f, 0.f};
+  for (;;) {
+    if (!alive) {
+      if (i >= np) break;
+      // pointLightRayGen (photon-mapping/cuda/deviceCode.cu:54-72)
+      const int64_t g = g_lo + i;
+      int l = 0;
+      while (l < nl - 1 && g >= loff[l + 1]) l++;
+      const uint32_t id = (uint32_t)(g - loff[l]);
+      const LightDev L = lights[l];
+      rng = lcg_init(id, 0u);
+      color = {L.rgb.x, L.rgb.y, L.rgb.z};
+      o = {L.pos.x, L.pos.y, L.pos.z};
+      d = random_point_in_unit_sphere(rng);
+      n = 0;
+      b = 0;
+      alive = true;
+    }
+    // one owl::traceRay + triangleMeshClosestHit (deviceCode.cu:113-131)
     Ray r;
     ray_prep(r, o, d);
     const HitInfo h = traverse<false>(S, r, tmin, kPhotonTmax, st, kTBlock, overflow);
@@ -76,8 +92,8 @@ __global__ __launch_bounds__(kTBlock) void k_trace_photons(DevScene S, const Lig
         ev = EV_ABSORBED;
       }
     }
-    const bool deposit = (b > 0) && (ev == EV_DIFFUSE);
-    if (deposit) {
+    // shootPhoton / shootCausticsPhoton deposit + continuation (deviceCode.cu:25-52)
+    if (b > 0 && ev == EV_DIFFUSE) {
       pm_photon p;
       p.pos = {so.x, so.y, so.z};
       p.dir = {sd.x, sd.y, sd.z};
@@ -87,12 +103,17 @@ __global__ __launch_bounds__(kTBlock) void k_trace_photons(DevScene S, const Lig
       n++;
     }
     const bool cont = caustic ? ((ev & (EV_SPECULAR | EV_REFRACT)) != 0) : (ev == EV_DIFFUSE);
-    if (!cont) break;
-    o = so;
-    d = sd;
-    color = sc;
+    b++;
+    if (!cont || b >= maxd) {
+      cnt[i] = n;
+      alive = false;
+      i += stride;
+    } else {
+      o = so;
+      d = sd;
+      color = sc;
+    }
   }
-  cnt[i] = n;
 }
 
 __global__ void k_compact_photons(const pm_photon* slots, const uint32_t* cnt, const uint32_t* off, int64_t np,
@@ -106,8 +127,10 @@ __global__ void k_compact_photons(const pm_photon* slots, const uint32_t* cnt, c
 hipError_t launch_trace_chunk(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl, int64_t g_lo,
                               int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt, hipStream_t s) {
   if (np <= 0) return hipSuccess;
-  k_trace_photons<<<grid_for(np, kTBlock), kTBlock, 0, s>>>(sc->view(), d_lights, d_loff, nl, g_lo, np, maxd,
-                                                             caustic, slots, cnt, sc->overflow.p);
+  if (maxd <= 0) return hipMemsetAsync(cnt, 0, sizeof(uint32_t) * np, s);
+  const int blocks = grid_for((np + kPhotonsPerLane - 1) / kPhotonsPerLane, kTBlock);
+  k_trace_photons<<<blocks, kTBlock, 0, s>>>(sc->view(), d_lights, d_loff, nl, g_lo, np, maxd, caustic, slots, cnt,
+                                             sc->overflow.p);
   return hipGetLastError();
 }
 
