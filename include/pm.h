@@ -121,9 +121,9 @@ int pm_last_phase_us(int32_t phase, double* us);
 typedef struct pm_scene pm_scene;
 typedef struct {
   int64_t num_triangles;
-  int64_t num_nodes;
+  int64_t num_nodes;          /* BVH4 nodes (collapsed from the binary LBVH) */
   int32_t num_meshes;
-  int32_t max_depth;          /* deepest BVH leaf */
+  int32_t max_depth;          /* BVH4 levels */
   pm_box bounds;
 } pm_scene_stats;
 

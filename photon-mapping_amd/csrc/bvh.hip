@@ -5,7 +5,8 @@
 // behind every owl::traceRay / optixTrace. Pipeline: 30-bit Morton codes of
 // triangle centroids -> stable radix sort -> Karras hierarchy -> bottom-up
 // refit (agent-scope release/acquire hand-off between sibling threads) into
-// 64-B BVH2 nodes that carry both child boxes (one node fetch = both tests).
+// 64-B BVH2 nodes that carry both child boxes -> greedy top-down collapse into
+// 128-B BVH4 nodes (one cache line = four box tests), which the traversal uses.
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -149,16 +150,119 @@ __global__ void k_pack_children(float4* nodes, const int4* child, int nn) {
   nodes[4 * i + 3] = *reinterpret_cast<const float4*>(&child[i]);
 }
 
-__global__ void k_leaf_depth(const int* parent_int, const int* parent_leaf, int n, int* maxdepth) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int d = 1;
-  int p = parent_leaf[i];
-  while (p != 0 && d < (1 << 20)) {
-    p = parent_int[p];
-    d++;
+// ---------------------------------------------------------------- BVH4 collapse
+// The binary LBVH is collapsed top-down into 4-wide nodes (128 B, one cache
+// line: SoA child boxes + 4 child codes). A BVH4 node adopts the two children
+// of its binary node, then repeatedly opens the internal candidate with the
+// largest surface area until it holds 4 (Wald et al. 2008 style greedy
+// collapse). One level of the BVH4 per launch pair; node ids are assigned by
+// an exclusive scan so the layout is deterministic.
+__device__ __forceinline__ float box_area(const float b[6]) {
+  const float dx = b[1] - b[0], dy = b[3] - b[2], dz = b[5] - b[4];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+__global__ void k_collapse_open(const float4* __restrict__ bin, const int2* __restrict__ frontier, int nf,
+                                float4* __restrict__ q, uint32_t* __restrict__ cnt) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nf) return;
+  const int2 fr = frontier[f];
+  int code[4];
+  float box[4][6];
+  const float* nb = reinterpret_cast<const float*>(&bin[4 * fr.x]);
+  const int4 c2 = *reinterpret_cast<const int4*>(&bin[4 * fr.x + 3]);
+  code[0] = c2.x;
+  code[1] = c2.y;
+#pragma unroll
+  for (int k = 0; k < 6; k++) box[0][k] = nb[k], box[1][k] = nb[6 + k];
+  int m = 2;
+  for (int it = 0; it < 2; it++) {
+    int best = -1;
+    float barea = -1.0f;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      if (c < m && code[c] >= 0) {
+        const float a = box_area(box[c]);
+        if (a > barea) barea = a, best = c;
+      }
+    }
+    if (best < 0) break;
+    const float* ob = reinterpret_cast<const float*>(&bin[4 * code[best]]);
+    const int4 oc = *reinterpret_cast<const int4*>(&bin[4 * code[best] + 3]);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      if (c == best) {
+        code[c] = oc.x;
+#pragma unroll
+        for (int k = 0; k < 6; k++) box[c][k] = ob[k];
+      } else if (c == m) {
+        code[c] = oc.y;
+#pragma unroll
+        for (int k = 0; k < 6; k++) box[c][k] = ob[6 + k];
+      }
+    }
+    m++;
   }
-  atomicMax(maxdepth, d);
+  uint32_t internal = 0;
+  float* qn = reinterpret_cast<float*>(&q[8 * (int64_t)fr.y]);
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const bool used = c < m;
+    if (used && code[c] >= 0) internal++;
+#pragma unroll
+    for (int k = 0; k < 6; k++) qn[4 * k + c] = used ? box[c][k] : 0.0f;   // k: lo.x hi.x lo.y hi.y lo.z hi.z
+    reinterpret_cast<int*>(qn)[24 + c] = used ? code[c] : kBvhEmpty;       // patched by k_collapse_link
+    reinterpret_cast<int*>(qn)[28 + c] = 0;
+  }
+  cnt[f] = internal;
+}
+
+__global__ void k_collapse_link(const int2* __restrict__ frontier, int nf, const uint32_t* __restrict__ off,
+                                int base, float4* __restrict__ q, int2* __restrict__ next) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nf) return;
+  const int2 fr = frontier[f];
+  int4* cp = reinterpret_cast<int4*>(&q[8 * (int64_t)fr.y + 6]);
+  int4 c = *cp;
+  int o = (int)off[f];
+  int* cc = reinterpret_cast<int*>(&c);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (cc[k] >= 0) {
+      next[o] = make_int2(cc[k], base + o);
+      cc[k] = base + o;
+      o++;
+    }
+  }
+  *cp = c;
+}
+
+static hipError_t collapse_bvh4(const float4* bin, int nbin, pm_scene* sc, hipStream_t s) {
+  sc->nodes.alloc((size_t)8 * nbin);
+  DevBuf<int2> fa(nbin), fb(nbin);
+  DevBuf<uint32_t> cnt(nbin), off(nbin), total(1);
+  if (!sc->nodes.p || !fa.p || !fb.p || !cnt.p || !off.p || !total.p) return hipErrorOutOfMemory;
+  const int2 root = make_int2(0, 0);
+  PM_HIP_TRY(hipMemcpyAsync(fa.p, &root, sizeof(int2), hipMemcpyHostToDevice, s));
+  int nf = 1, alloc = 1, depth = 0;
+  int2 *cur = fa.p, *nxt = fb.p;
+  while (nf > 0) {
+    depth++;
+    k_collapse_open<<<grid_for(nf, 256), 256, 0, s>>>(bin, cur, nf, sc->nodes.p, cnt.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(exclusive_scan_u32(cnt.p, off.p, nf, total.p, s));
+    k_collapse_link<<<grid_for(nf, 256), 256, 0, s>>>(cur, nf, off.p, alloc, sc->nodes.p, nxt);
+    PM_HIP_TRY(hipGetLastError());
+    uint32_t t = 0;
+    PM_HIP_TRY(hipMemcpyAsync(&t, total.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    alloc += (int)t;
+    nf = (int)t;
+    std::swap(cur, nxt);
+  }
+  sc->nnodes = alloc;
+  sc->depth = depth;
+  return hipSuccess;
 }
 
 hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s) {
@@ -193,10 +297,9 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s
   DevBuf<float4> tri_orig((size_t)3 * n);
   sc->tri.alloc((size_t)3 * n);
   const int nn = std::max(1, n - 1);
-  sc->nodes.alloc((size_t)4 * nn);
-  if (!tri_orig.p || !sc->tri.p || !sc->nodes.p) return hipErrorOutOfMemory;
+  DevBuf<float4> bin((size_t)4 * nn);   // binary LBVH, collapsed into sc->nodes below
+  if (!tri_orig.p || !sc->tri.p || !bin.p) return hipErrorOutOfMemory;
   PM_HIP_TRY(hipMemcpyAsync(tri_orig.p, th.data(), sizeof(float4) * 3 * n, hipMemcpyHostToDevice, s));
-  sc->nnodes = nn;
   if (n == 1) {
     PM_HIP_TRY(hipMemcpyAsync(sc->tri.p, tri_orig.p, sizeof(float4) * 3, hipMemcpyDeviceToDevice, s));
     const float4 a = th[0], b = th[1], c = th[2];
@@ -207,16 +310,14 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s
     for (int k = 0; k < 6; k++) node[k] = bx[k], node[6 + k] = bx[k];
     const int ch[4] = {~0, ~0, 0, 0};
     std::memcpy(&node[12], ch, 16);
-    PM_HIP_TRY(hipMemcpyAsync(sc->nodes.p, node, 64, hipMemcpyHostToDevice, s));
-    PM_HIP_TRY(hipStreamSynchronize(s));
-    sc->depth = 1;
-    return hipSuccess;
+    PM_HIP_TRY(hipMemcpyAsync(bin.p, node, 64, hipMemcpyHostToDevice, s));
+    return collapse_bvh4(bin.p, nn, sc, s);
   }
   DevBuf<uint32_t> codes(n), order(n);
   DevBuf<int4> child(nn);
-  DevBuf<int> pint(nn), pleaf(n), depth(1);
+  DevBuf<int> pint(nn), pleaf(n);
   DevBuf<unsigned> flags(nn);
-  if (!codes.p || !order.p || !child.p || !pint.p || !pleaf.p || !flags.p || !depth.p) return hipErrorOutOfMemory;
+  if (!codes.p || !order.p || !child.p || !pint.p || !pleaf.p || !flags.p) return hipErrorOutOfMemory;
   float3 clo3 = make_float3(clo[0], clo[1], clo[2]);
   float3 inv = make_float3(chi[0] > clo[0] ? 1.0f / (chi[0] - clo[0]) : 0.f,
                            chi[1] > clo[1] ? 1.0f / (chi[1] - clo[1]) : 0.f,
@@ -230,18 +331,11 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s
   k_hierarchy<<<grid_for(n - 1, 256), 256, 0, s>>>(codes.p, n, child.p, pint.p, pleaf.p);
   PM_HIP_TRY(hipGetLastError());
   PM_HIP_TRY(hipMemsetAsync(flags.p, 0, sizeof(unsigned) * nn, s));
-  k_refit<<<grid_for(n, 256), 256, 0, s>>>(sc->tri.p, n, pad, sc->nodes.p, child.p, pint.p, pleaf.p, flags.p);
+  k_refit<<<grid_for(n, 256), 256, 0, s>>>(sc->tri.p, n, pad, bin.p, child.p, pint.p, pleaf.p, flags.p);
   PM_HIP_TRY(hipGetLastError());
-  k_pack_children<<<grid_for(nn, 256), 256, 0, s>>>(sc->nodes.p, child.p, nn);
+  k_pack_children<<<grid_for(nn, 256), 256, 0, s>>>(bin.p, child.p, nn);
   PM_HIP_TRY(hipGetLastError());
-  PM_HIP_TRY(hipMemsetAsync(depth.p, 0, sizeof(int), s));
-  k_leaf_depth<<<grid_for(n, 256), 256, 0, s>>>(pint.p, pleaf.p, n, depth.p);
-  PM_HIP_TRY(hipGetLastError());
-  int dh = 0;
-  PM_HIP_TRY(hipMemcpyAsync(&dh, depth.p, sizeof(int), hipMemcpyDeviceToHost, s));
-  PM_HIP_TRY(hipStreamSynchronize(s));
-  sc->depth = dh;
-  return hipSuccess;
+  return collapse_bvh4(bin.p, nn, sc, s);
 }
 
 // ---------------------------------------------------------------- queries

@@ -167,10 +167,10 @@ __device__ __forceinline__ float schlick(float cosv, float ior) {
 
 // ---------------------------------------------------------------- scene
 // Triangle record (48 B, 3 x float4): A.xyz|mesh, B.xyz|prim, C.xyz|global tri id.
-// BVH2 node (64 B): left box, right box, child ids (>=0 internal, <0 leaf ~slot).
+// BVH4 node (128 B): SoA boxes of 4 children + child codes (see traverse).
 struct DevScene {
   const float4* tri;       // [3*T] in leaf (Morton) order
-  const float4* nodes;     // [4*(T-1)] or 1 node for T == 1
+  const float4* nodes;     // [8 * nnodes] BVH4
   const float4* mat;       // [2*nmesh]: (albedo, diffuse), (specular, transmission, ior, 0)
   int32_t ntri;
   int32_t nnodes;
@@ -258,7 +258,17 @@ __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, flo
   return tn <= tf;
 }
 
-constexpr int kStackDepth = 64;
+// Traversal stack: the top kStackDepth entries live in LDS ([depth][blockDim],
+// sized for occupancy: 16 x 4 B x 64 lanes = 4 KB per wave); deeper entries
+// spill to a per-lane private (scratch) array that only deep paths touch.
+// A BVH4 of depth D needs at most 3 (D - 1) entries, so scenes with D <= 22
+// can never overflow; deeper ones report PM_ERR_OVERFLOW if a ray does.
+#ifndef PM_STACK_DEPTH
+#define PM_STACK_DEPTH 16
+#endif
+constexpr int kStackDepth = PM_STACK_DEPTH;
+constexpr int kSpillDepth = 64 - PM_STACK_DEPTH > 0 ? 64 - PM_STACK_DEPTH : 1;
+constexpr int32_t kBvhEmpty = INT32_MIN;
 
 // Bottom levels of a left-balanced kd-tree stored subtree-contiguously: node t
 // >= first is a bucket root whose subtree (level order, `slots` = 2^B - 1
@@ -277,74 +287,99 @@ struct HitInfo {
 
 // Closest hit in (tmin, tmax): argmin (t, global triangle index). `stack`
 // points at this lane's column of an LDS stack laid out [depth][blockDim].
+// BVH4 node (8 x float4): lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4]
+// codes[4] (>= 0 internal node, kBvhEmpty unused, else ~triangle slot), pad.
+__device__ __forceinline__ void cas(float& ta, int& ca, float& tb, int& cb) {
+  const bool sw = tb < ta;
+  const float t = sw ? tb : ta;
+  tb = sw ? ta : tb;
+  ta = t;
+  const int c = sw ? cb : ca;
+  cb = sw ? ca : cb;
+  ca = c;
+}
+
+template <bool ANY>
+__device__ __forceinline__ bool leaf_test(const DevScene& S, const Ray& r, float tmin, float tmax, int code,
+                                          HitInfo& h) {
+  const int slot = ~code;
+  const float4 a = S.tri[3 * slot + 0];
+  const float4 b = S.tri[3 * slot + 1];
+  const float4 c = S.tri[3 * slot + 2];
+  float t;
+  if (wt_hit(a, b, c, r, t) && t > tmin && t < tmax) {
+    const int gid = __float_as_int(c.w);
+    if (ANY || h.slot < 0 || t < h.t || (t == h.t && gid < h.gid)) {
+      h.t = t;
+      h.slot = slot;
+      h.gid = gid;
+      return true;
+    }
+  }
+  return false;
+}
+
 template <bool ANY>
 __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
                                             int stride, int* overflow) {
   HitInfo h{tmax, -1, -1};
   if (S.ntri <= 0) return h;
+  int spill[kSpillDepth];
   int sp = 0;
   int node = 0;
   for (;;) {
-    const float4 n0 = S.nodes[4 * node + 0];
-    const float4 n1 = S.nodes[4 * node + 1];
-    const float4 n2 = S.nodes[4 * node + 2];
-    const int4 n3 = *reinterpret_cast<const int4*>(&S.nodes[4 * node + 3]);
+    const float4* q = S.nodes + 8 * (int64_t)node;
+    const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+    const int4 ch = *reinterpret_cast<const int4*>(&q[6]);
     const float lim = (ANY || h.slot < 0) ? tmax * 1.00001f : h.t * 1.00001f;
-    float tnl, tnr;
-    const bool hl = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, tmin, lim, tnl);
-    const bool hr = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, tmin, lim, tnr);
-    int next = -1;
-    // near child first: visit order only changes speed (closest hit is the
-    // argmin over (t, id) regardless of order)
-    const bool swap = !ANY && hl && hr && tnr < tnl;
-    int cand[2] = {hl ? n3.x : INT32_MAX, hr ? n3.y : INT32_MAX};
-    if (swap) {
-      const int t = cand[0];
-      cand[0] = cand[1];
-      cand[1] = t;
-    }
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-      const int ch = cand[c];
-      if (ch == INT32_MAX) continue;
-      if (ch < 0) {
-        const int slot = ~ch;
-        const float4 a = S.tri[3 * slot + 0];
-        const float4 b = S.tri[3 * slot + 1];
-        const float4 cc = S.tri[3 * slot + 2];
-        float t;
-        if (wt_hit(a, b, cc, r, t) && t > tmin && t < tmax) {
-          const int gid = __float_as_int(cc.w);
-          if (ANY) {
-            h.t = t;
-            h.slot = slot;
-            h.gid = gid;
-            return h;
-          }
-          if (h.slot < 0 || t < h.t || (t == h.t && gid < h.gid)) {
-            h.t = t;
-            h.slot = slot;
-            h.gid = gid;
-          }
-        }
-      } else if (next < 0) {
-        next = ch;
+    float t0, t1, t2, t3;
+    const bool b0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, tmin, lim, t0) && ch.x != kBvhEmpty;
+    const bool b1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tmin, lim, t1) && ch.y != kBvhEmpty;
+    const bool b2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tmin, lim, t2) && ch.z != kBvhEmpty;
+    const bool b3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tmin, lim, t3) && ch.w != kBvhEmpty;
+    // leaves first: a hit shrinks the limit applied to the internal children
+    if (b0 && ch.x < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.x, h) && ANY) return h;
+    if (b1 && ch.y < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.y, h) && ANY) return h;
+    if (b2 && ch.z < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.z, h) && ANY) return h;
+    if (b3 && ch.w < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.w, h) && ANY) return h;
+    const float lim2 = (ANY || h.slot < 0) ? lim : h.t * 1.00001f;
+    // internal children hit within the (possibly tightened) limit, sorted
+    // near-to-far: order only changes speed, the result is argmin (t, id)
+    float k0 = (b0 && ch.x >= 0 && t0 <= lim2) ? t0 : INFINITY;
+    float k1 = (b1 && ch.y >= 0 && t1 <= lim2) ? t1 : INFINITY;
+    float k2 = (b2 && ch.z >= 0 && t2 <= lim2) ? t2 : INFINITY;
+    float k3 = (b3 && ch.w >= 0 && t3 <= lim2) ? t3 : INFINITY;
+    const int cnt = (k0 != INFINITY) + (k1 != INFINITY) + (k2 != INFINITY) + (k3 != INFINITY);
+    int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+    cas(k0, c0, k1, c1);
+    cas(k2, c2, k3, c3);
+    cas(k0, c0, k2, c2);
+    cas(k1, c1, k3, c3);
+    cas(k1, c1, k2, c2);
+    if (cnt > 0) {
+      if (sp + cnt - 1 > kStackDepth + kSpillDepth) {
+        *overflow = 1;
+      } else if (sp + cnt - 1 <= kStackDepth) {
+        if (cnt > 3) stack[(sp++) * stride] = c3;
+        if (cnt > 2) stack[(sp++) * stride] = c2;
+        if (cnt > 1) stack[(sp++) * stride] = c1;
       } else {
-        if (sp < kStackDepth) {
-          stack[sp * stride] = ch;
-          sp++;
-        } else {
-          *overflow = 1;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          const int c = k == 0 ? c3 : (k == 1 ? c2 : c1);
+          if (k >= 4 - cnt) {
+            if (sp < kStackDepth) stack[sp * stride] = c;
+            else spill[sp - kStackDepth] = c;
+            sp++;
+          }
         }
       }
-    }
-    if (next >= 0) {
-      node = next;
+      node = c0;
       continue;
     }
     if (sp == 0) break;
     sp--;
-    node = stack[sp * stride];
+    node = sp < kStackDepth ? stack[sp * stride] : spill[sp - kStackDepth];
   }
   return h;
 }

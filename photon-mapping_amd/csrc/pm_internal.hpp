@@ -10,10 +10,10 @@
 #include "pm_device.hpp"
 #include "prims.hpp"
 
-// Device-resident scene: triangles in BVH leaf order + LBVH2 nodes + materials.
+// Device-resident scene: triangles in BVH leaf order + BVH4 nodes + materials.
 struct pm_scene {
   pmd::DevBuf<float4> tri;      // 3 per triangle
-  pmd::DevBuf<float4> nodes;    // 4 per internal node
+  pmd::DevBuf<float4> nodes;    // 8 per BVH4 node
   pmd::DevBuf<float4> mat;      // 2 per mesh
   pmd::DevBuf<int32_t> overflow;
   int32_t ntri = 0, nnodes = 0, nmesh = 0, depth = 0;

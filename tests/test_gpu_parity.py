@@ -72,8 +72,9 @@ def test_scene_stats(sphere):
     meshes, _ = sphere
     s = pm_amd.Scene(meshes).stats()
     assert s.num_triangles == sum(len(m.indices) for m in meshes)
-    assert s.num_nodes == s.num_triangles - 1
-    assert 0 < s.max_depth <= 64
+    # BVH4 collapsed from a binary LBVH with T - 1 internal nodes
+    assert (s.num_triangles - 1) // 3 <= s.num_nodes <= s.num_triangles - 1
+    assert 0 < s.max_depth <= 32
 
 
 @pytest.mark.parametrize("which,casted", [("cornell", 10000), ("sphere", 100000)])
