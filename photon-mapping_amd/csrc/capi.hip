@@ -382,7 +382,6 @@ int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_phot
       PhaseTimer tm(PH_KDBUILD, s);
       e = launch_elems_from_photons(a, na, b, nb, pa, pb, elems.p, m->payload.p, s);
       if (e == hipSuccess) e = kd_build(elems.p, n, m->nodes.p, s);
-      if (e == hipSuccess) e = kd_make_buckets(m, s);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {

@@ -10,8 +10,8 @@
 // dimension (stable radix sort on (coord, index)); every level then splits each
 // active subtree range at its left-balanced median — the median element is read
 // directly from the list of the chosen dimension and the three lists are
-// stably partitioned around it with one fused flag pass, one u64 scan and one
-// scatter. Subtree ranges are identical in the three lists, so a single tag
+// stably partitioned around it (segmented count scan over 1024-position tiles:
+// k_kd_count -> k_kd_tilescan -> k_kd_part). Subtree ranges are identical in the three lists, so a single tag
 // array tracks subtree membership. Ties are broken by the original index.
 #include <algorithm>
 #include <cstdlib>
@@ -100,66 +100,198 @@ __device__ __forceinline__ int kd_class(const float4 e, int dim, float nc, int n
   return 2;
 }
 
-__global__ void k_kd_flags(const float4* l0, const float4* l1, const float4* l2, const int32_t* tag, int64_t n,
-                           SegTab T, uint64_t* flags) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const int t = tag[p];
-  if (t < 0) {
-    flags[p] = 0;
-    flags[n + p] = 0;
-    flags[2 * n + p] = 0;
-    return;
-  }
-  const int dim = T.dim[t];
-  const float nc = T.coord[t];
-  const int nid = T.id[t];
-  const float4 e[3] = {l0[p], l1[p], l2[p]};
-#pragma unroll
-  for (int d = 0; d < 3; d++) {
-    const int c = kd_class(e[d], dim, nc, nid);
-    flags[(int64_t)d * n + p] = c == 0 ? 1ull : (c == 2 ? (1ull << 32) : 0ull);
-  }
+// ------------------------------------------------------------------ partition
+// Per level (replaces flags -> u64 scan -> scatter -> tag): positions are cut
+// into 1024-position tiles; the element at each position of the three lists is
+// classed against its segment's median (L / M / R / already placed) and the
+// packed (L, R) counts are scanned SEGMENTED (reset at segment starts):
+//   k_kd_count     per-tile segmented aggregate,
+//   k_kd_tilescan  one block: exclusive segmented carry per tile,
+//   k_kd_part      block scan + carry -> stable scatter: L -> b + #L before it
+//                  in the segment, M -> b + ls, R -> b + ls + 1 + #R before it;
+//                  the tag (segment id per position) is updated in place.
+// Kernel boundaries order the passes (a decoupled look-back needs agent-scope
+// release fences per tile, i.e. L2 write-backs across the 8 XCDs: measured
+// 7 ms per level). Traffic per element and level: 2 x (3 x 16 B + 4 B) read,
+// 3 x 16 B + 4 B written.
+constexpr int kPartThreads = 256;
+constexpr int kPartIPT = 4;
+constexpr int kPartTile = kPartThreads * kPartIPT;   // positions per tile
+
+struct SegVal {   // segmented-scan value: packed (L | R << 32) count per list
+  uint64_t v[3];
+  uint32_t f;     // contains a segment start
+};
+
+__device__ __forceinline__ SegVal seg_zero() {
+  SegVal r;
+  r.v[0] = r.v[1] = r.v[2] = 0;
+  r.f = 0;
+  return r;
 }
 
-__global__ void k_kd_scatter(const float4* l0, const float4* l1, const float4* l2, float4* o0, float4* o1, float4* o2,
-                             const int32_t* tag, int64_t n, SegTab T, const uint64_t* pre) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const int t = tag[p];
+__device__ __forceinline__ SegVal seg_combine(const SegVal& a, const SegVal& b) {   // a before b
+  SegVal r;
+#pragma unroll
+  for (int d = 0; d < 3; d++) r.v[d] = b.f ? b.v[d] : a.v[d] + b.v[d];
+  r.f = a.f | b.f;
+  return r;
+}
+
+__device__ __forceinline__ SegVal seg_shfl_up(const SegVal& x, int delta) {
+  SegVal r;
+#pragma unroll
+  for (int d = 0; d < 3; d++) r.v[d] = __shfl_up(x.v[d], delta);
+  r.f = (uint32_t)__shfl_up((int)x.f, delta);
+  return r;
+}
+
+// Block-wide exclusive segmented scan (blockDim = W * 64); also returns the
+// block aggregate. `sh` holds W entries.
+template <int W>
+__device__ __forceinline__ SegVal block_seg_scan(const SegVal& th, SegVal* sh, SegVal& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  SegVal inc = th;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const SegVal up = seg_shfl_up(inc, o);
+    if (lane >= o) inc = seg_combine(up, inc);
+  }
+  if (lane == 63) sh[wave] = inc;
+  __syncthreads();
+  SegVal ex = seg_shfl_up(inc, 1);
+  if (lane == 0) ex = seg_zero();
+  SegVal wpre = seg_zero();
+  total = seg_zero();
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    if (w < wave) wpre = seg_combine(wpre, sh[w]);
+    total = seg_combine(total, sh[w]);
+  }
+  __syncthreads();   // sh is reused by the next call
+  return seg_combine(wpre, ex);
+}
+
+// Striped tiles: item k of thread i sits at position tile*1024 + k*256 + i, so
+// every list load / scatter store of a wave covers 1 KB of consecutive
+// positions; the segmented scan runs once per k-round, carried across rounds.
+struct PartItem {
+  int tg, sb, sls;
+  uint8_t cls[3];   // 0 L, 1 M, 2 R, 3 placed / out of range
+};
+
+template <bool KEEP>
+__device__ __forceinline__ SegVal part_load(const float4* __restrict__ l0, const float4* __restrict__ l1,
+                                            const float4* __restrict__ l2, const int32_t* __restrict__ tag,
+                                            int64_t n, const SegTab& T, int64_t p, PartItem& it, float4 (&e)[3]) {
   const float4* L[3] = {l0, l1, l2};
-  float4* O[3] = {o0, o1, o2};
-  if (t < 0) {
-#pragma unroll
-    for (int d = 0; d < 3; d++) O[d][p] = L[d][p];
-    return;
+  SegVal th = seg_zero();
+  it.tg = p < n ? tag[p] : -1;
+  int dim = 0, nid = 0;
+  float nc = 0.f;
+  it.sb = 0;
+  it.sls = 0;
+  if (it.tg >= 0) {
+    const int t = it.tg;
+    it.sb = T.b[t];
+    it.sls = T.ls[t];
+    dim = T.dim[t];
+    nc = T.coord[t];
+    nid = T.id[t];
   }
-  const int b = T.b[t], ls = T.ls[t], dim = T.dim[t];
-  const float nc = T.coord[t];
-  const int nid = T.id[t];
+  th.f = it.tg >= 0 && p == it.sb;
 #pragma unroll
   for (int d = 0; d < 3; d++) {
-    const float4 e = L[d][p];
-    const int c = kd_class(e, dim, nc, nid);
-    const uint64_t pp = pre[(int64_t)d * n + p], pb = pre[(int64_t)d * n + b];
-    int64_t np;
-    if (c == 0)
-      np = b + (int64_t)((uint32_t)pp - (uint32_t)pb);
-    else if (c == 1)
-      np = b + ls;
-    else
-      np = b + ls + 1 + (int64_t)((uint32_t)(pp >> 32) - (uint32_t)(pb >> 32));
-    O[d][np] = e;
+    const float4 x = p < n ? L[d][p] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (KEEP) e[d] = x;
+    const int c = it.tg < 0 ? 3 : kd_class(x, dim, nc, nid);
+    it.cls[d] = (uint8_t)c;
+    th.v[d] = c == 0 ? 1ull : (c == 2 ? (1ull << 32) : 0ull);
+  }
+  return th;
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_kd_count(const float4* __restrict__ l0,
+                                                           const float4* __restrict__ l1,
+                                                           const float4* __restrict__ l2,
+                                                           const int32_t* __restrict__ tag, int64_t n, SegTab T,
+                                                           SegVal* __restrict__ tile_agg) {
+  __shared__ SegVal sh[kPartThreads / 64];
+  const int64_t base = (int64_t)blockIdx.x * kPartTile + threadIdx.x;
+  SegVal th[kPartIPT];
+  float4 dummy[3];
+#pragma unroll
+  for (int k = 0; k < kPartIPT; k++) {
+    PartItem it;
+    th[k] = part_load<false>(l0, l1, l2, tag, n, T, base + k * kPartThreads, it, dummy);
+  }
+  SegVal agg = seg_zero();
+#pragma unroll
+  for (int k = 0; k < kPartIPT; k++) {
+    SegVal total;
+    block_seg_scan<kPartThreads / 64>(th[k], sh, total);
+    agg = seg_combine(agg, total);
+  }
+  if (threadIdx.x == 0) tile_agg[blockIdx.x] = agg;
+}
+
+// One block: exclusive segmented prefix over the tile aggregates.
+constexpr int kTileScanThreads = 1024;
+__global__ __launch_bounds__(kTileScanThreads) void k_kd_tilescan(const SegVal* __restrict__ agg, int64_t ntiles,
+                                                                  SegVal* __restrict__ carry) {
+  __shared__ SegVal sh[kTileScanThreads / 64];
+  const int64_t per = (ntiles + kTileScanThreads - 1) / kTileScanThreads;
+  const int64_t t0 = (int64_t)threadIdx.x * per, t1 = min(ntiles, t0 + per);
+  SegVal th = seg_zero();
+  for (int64_t t = t0; t < t1; t++) th = seg_combine(th, agg[t]);
+  SegVal total;
+  SegVal run = block_seg_scan<kTileScanThreads / 64>(th, sh, total);
+  for (int64_t t = t0; t < t1; t++) {
+    carry[t] = run;
+    run = seg_combine(run, agg[t]);
   }
 }
 
-__global__ void k_kd_tag(int32_t* tag, int64_t n, SegTab T) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const int t = tag[p];
-  if (t < 0) return;
-  const int mid = T.b[t] + T.ls[t];
-  tag[p] = p < mid ? 2 * t + 1 : (p == mid ? -1 : 2 * t + 2);
+__global__ __launch_bounds__(kPartThreads) void k_kd_part(const float4* __restrict__ l0, const float4* __restrict__ l1,
+                                                          const float4* __restrict__ l2, float4* __restrict__ o0,
+                                                          float4* __restrict__ o1, float4* __restrict__ o2,
+                                                          int32_t* __restrict__ tag, int64_t n, SegTab T,
+                                                          const SegVal* __restrict__ tile_carry) {
+  __shared__ SegVal sh[kPartThreads / 64];
+  const int64_t base = (int64_t)blockIdx.x * kPartTile + threadIdx.x;
+  float4* O[3] = {o0, o1, o2};
+  PartItem it[kPartIPT];
+  float4 e[kPartIPT][3];
+  SegVal th[kPartIPT];
+#pragma unroll
+  for (int k = 0; k < kPartIPT; k++)
+    th[k] = part_load<true>(l0, l1, l2, tag, n, T, base + k * kPartThreads, it[k], e[k]);
+  SegVal carry = tile_carry[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kPartIPT; k++) {
+    SegVal total;
+    const SegVal ex = block_seg_scan<kPartThreads / 64>(th[k], sh, total);
+    SegVal run = seg_combine(carry, ex);   // counts before this position in its segment
+    carry = seg_combine(carry, total);
+    const int64_t p = base + k * kPartThreads;
+    if (p >= n) continue;
+    if (th[k].f) run = seg_zero();
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const int c = it[k].cls[d];
+      int64_t dst;
+      if (c == 3) dst = p;
+      else if (c == 0) dst = it[k].sb + (int64_t)(uint32_t)run.v[d];
+      else if (c == 1) dst = it[k].sb + it[k].sls;
+      else dst = it[k].sb + it[k].sls + 1 + (int64_t)(uint32_t)(run.v[d] >> 32);
+      O[d][dst] = e[k][d];
+    }
+    if (it[k].tg >= 0) {
+      const int t = it[k].tg;
+      const int64_t mid = it[k].sb + it[k].sls;
+      tag[p] = p < mid ? 2 * t + 1 : (p == mid ? -1 : 2 * t + 2);
+    }
+  }
 }
 
 hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s) {
@@ -187,8 +319,9 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
   }
   DevBuf<int32_t> tb(cap), ts(cap), tls(cap), tdim(cap), tid(cap), tag(n);
   DevBuf<float> tco(cap);
-  DevBuf<uint64_t> flags((size_t)3 * n), pre((size_t)3 * n);
-  if (!tb.p || !ts.p || !tls.p || !tdim.p || !tid.p || !tag.p || !tco.p || !flags.p || !pre.p)
+  const int64_t ntiles = (n + kPartTile - 1) / kPartTile;
+  DevBuf<SegVal> tagg(ntiles), tcarry(ntiles);
+  if (!tb.p || !ts.p || !tls.p || !tdim.p || !tid.p || !tag.p || !tco.p || !tagg.p || !tcarry.p)
     return hipErrorOutOfMemory;
   SegTab T{tb.p, ts.p, tls.p, tdim.p, tco.p, tid.p};
   const int32_t root[2] = {0, (int32_t)n};
@@ -202,13 +335,12 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
     k_kd_seg<<<grid_for(nseg, 256), 256, 0, s>>>(cur[0], cur[1], cur[2], L, cap, T, nodes);
     PM_HIP_TRY(hipGetLastError());
     if (L == H - 1) break;   // last level: every remaining subtree has one node
-    k_kd_flags<<<grid_for(n, 256), 256, 0, s>>>(cur[0], cur[1], cur[2], tag.p, n, T, flags.p);
+    k_kd_count<<<(int)ntiles, kPartThreads, 0, s>>>(cur[0], cur[1], cur[2], tag.p, n, T, tagg.p);
     PM_HIP_TRY(hipGetLastError());
-    PM_HIP_TRY(exclusive_scan_u64(flags.p, pre.p, 3 * n, nullptr, s));
-    k_kd_scatter<<<grid_for(n, 256), 256, 0, s>>>(cur[0], cur[1], cur[2], nxt[0], nxt[1], nxt[2], tag.p, n, T,
-                                                   pre.p);
+    k_kd_tilescan<<<1, kTileScanThreads, 0, s>>>(tagg.p, ntiles, tcarry.p);
     PM_HIP_TRY(hipGetLastError());
-    k_kd_tag<<<grid_for(n, 256), 256, 0, s>>>(tag.p, n, T);
+    k_kd_part<<<(int)ntiles, kPartThreads, 0, s>>>(cur[0], cur[1], cur[2], nxt[0], nxt[1], nxt[2], tag.p, n, T,
+                                                   tcarry.p);
     PM_HIP_TRY(hipGetLastError());
     for (int d = 0; d < 3; d++) {
       float4* t = cur[d];
@@ -219,44 +351,6 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
   return hipSuccess;
 }
 
-// ---------------------------------------------------------------- buckets
-__global__ void k_kd_buckets(const float4* nodes, int64_t n, int first, int nb, int levels, float4* out) {
-  const int slots = (1 << levels) - 1;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)nb * slots) return;
-  const int64_t b = i / slots;
-  const int sl = (int)(i % slots);
-  const int lvl = 31 - __clz(sl + 1);            // level inside the subtree
-  const int j = sl + 1 - (1 << lvl);             // position in that level
-  const int64_t root = first + b;
-  const int64_t t = ((root + 1) << lvl) - 1 + j;  // implicit index of the node
-  out[i] = t < n ? nodes[t] : make_float4(INFINITY, INFINITY, INFINITY, __int_as_float(-1));
-}
-
-hipError_t kd_make_buckets(pm_photon_map* m, hipStream_t s) {
-  const int64_t n = m->n;
-  m->bucket_first = INT32_MAX;
-  m->bucket_slots = 0;
-  m->bucket_data.reset();
-  int B = kBucketLevels;
-  if (const char* e = std::getenv("PM_KD_BUCKET_LEVELS")) B = std::atoi(e);   // tuning knob; 0 = off
-  if (n <= 0 || B <= 0) return hipSuccess;
-  int H = 0;
-  while ((1ll << H) <= n) H++;                   // levels
-  const int lb = H > B ? H - B : 0;
-  const int levels = H - lb;
-  const int first = (1 << lb) - 1;
-  const int nb = (int)std::min<int64_t>(1ll << lb, std::max<int64_t>(0, n - first));
-  const int slots = (1 << levels) - 1;
-  m->bucket_data.alloc((size_t)nb * slots);
-  if (!m->bucket_data.p) return hipErrorOutOfMemory;
-  k_kd_buckets<<<grid_for((int64_t)nb * slots, 256), 256, 0, s>>>(m->nodes.p, n, first, nb, levels,
-                                                                 m->bucket_data.p);
-  PM_HIP_TRY(hipGetLastError());
-  m->bucket_first = first;
-  m->bucket_slots = slots;
-  return hipSuccess;
-}
 
 // ---------------------------------------------------------------- helpers for the C-ABI
 __global__ void k_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,

@@ -270,15 +270,6 @@ constexpr int kStackDepth = PM_STACK_DEPTH;
 constexpr int kSpillDepth = 64 - PM_STACK_DEPTH > 0 ? 64 - PM_STACK_DEPTH : 1;
 constexpr int32_t kBvhEmpty = INT32_MIN;
 
-// Bottom levels of a left-balanced kd-tree stored subtree-contiguously: node t
-// >= first is a bucket root whose subtree (level order, `slots` = 2^B - 1
-// entries, missing nodes = +inf sentinels) lives at data[(t - first) * slots].
-struct KdBuckets {
-  const float4* data;
-  int32_t first;     // INT32_MAX: no buckets
-  int32_t slots;
-};
-
 struct HitInfo {
   float t;
   int32_t slot;   // triangle slot (leaf order) or -1

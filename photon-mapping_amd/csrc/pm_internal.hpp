@@ -35,11 +35,7 @@ struct pm_scene {
 struct pm_photon_map {
   pmd::DevBuf<float4> nodes;
   pmd::DevBuf<float4> payload;
-  pmd::DevBuf<float4> bucket_data;   // bottom-level subtrees, contiguous (KdBuckets)
-  int32_t bucket_first = INT32_MAX;
-  int32_t bucket_slots = 0;
   int64_t n = 0;
-  pmd::KdBuckets buckets() const { return {bucket_data.p, bucket_first, bucket_slots}; }
 };
 
 namespace pmd {
@@ -61,9 +57,6 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& tri_host, hipStre
 // Core left-balanced kd-tree build over elements (x, y, z, bits(orig)).
 // Writes nodes[t] = (x, y, z, bits(orig << 2 | dim)).
 hipError_t kd_build(const float4* d_elems, int64_t n, float4* d_nodes, hipStream_t s);
-// Copy the bottom kLeafLevels levels of the tree into contiguous buckets.
-constexpr int kBucketLevels = 0;   // off: with Morton-sorted queries the pruned walk wins (r01 sweep)
-hipError_t kd_make_buckets(pm_photon_map* m, hipStream_t s);
 
 // K = 50 gather (gatherPhotons) for a batch of queries.
 // tag 0: API / caustic-map launches, 1: global-map launch (separate kernel symbol for rocprof)

@@ -141,7 +141,7 @@ def _check_left_balanced(pos, dims):
     return True
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 7, 1000, 65537, 300000])
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 1000, 65537, 300000, 2_000_003])
 def test_kdtree_build_left_balanced(n):
     import pm_amd
     rng = np.random.default_rng(n)
