@@ -94,8 +94,8 @@ def main():
     ap.add_argument("--scene", default="sponza", choices=["sponza", "cornell"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-sample-photons", type=int, default=200_000)
-    ap.add_argument("--cpu-sample-rows", type=int, default=8)
+    ap.add_argument("--cpu-sample-photons", type=int, default=2_000_000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=48)
     args = ap.parse_args()
 
     import torch
@@ -179,7 +179,12 @@ def main():
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("workload") == [args.scene, args.casted, args.caustic, args.width, args.height, args.spp]:
+            import hashlib
+            with open(pm_amd.LIB_PATH, "rb") as f:
+                lib_sha = hashlib.sha256(f.read()).hexdigest()
+            # only while the library is the one the counters were collected on
+            if pmc.get("workload") == [args.scene, args.casted, args.caustic, args.width, args.height, args.spp] \
+                    and pmc.get("lib_sha256") == lib_sha:
                 traffic = pmc.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -207,7 +212,7 @@ def main():
         "photon_maps": {"global": info["n_global"], "caustic": info["n_caustic"]},
         "render": {"path_vertices": int(st.path_vertices), "caustic_queries": int(st.caustic_queries),
                    "global_queries": nq_g, "rays": int(st.rays)},
-        "roofline": {"bound": "hbm", "kernel": "pmd::k_gather<1> (global-map kNN radiance estimate)",
+        "roofline": {"bound": "hbm", "kernel": "pmd::k_gather<1, true, 4> (global-map kNN radiance estimate)",
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "bytes_per_query": bpq, "queries_per_launch": nq_g,

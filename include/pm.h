@@ -116,6 +116,12 @@ int pm_device_count(int32_t* count);
  * 3 render-paths, 4 knn-gather (all), 5 resolve, 6 bvh-build, 7 the global-map
  * gather launch alone (the dominant kernel). */
 int pm_last_phase_us(int32_t phase, double* us);
+/* Device memory for callers without HIP headers (the CLI, cgo / JNI / ctypes
+ * bindings): hipMalloc / hipFree / synchronous hipMemcpy on the current device. */
+int pm_device_alloc(size_t bytes, void** d_ptr);
+int pm_device_free(void* d_ptr);
+int pm_copy_to_device(void* d_dst, const void* h_src, size_t bytes);
+int pm_copy_to_host(void* h_dst, const void* d_src, size_t bytes);
 
 /* ---- scene (world.cpp:3-58 loadGeometry; OptiX GAS+IAS -> HIP LBVH) ------- */
 typedef struct pm_scene pm_scene;

@@ -153,6 +153,33 @@ int pm_last_phase_us(int32_t phase, double* us) {
 }
 
 // ------------------------------------------------------------------ scene
+int pm_device_alloc(size_t bytes, void** d_ptr) {
+  if (!d_ptr) return PM_ERR_INVALID;
+  *d_ptr = nullptr;
+  if (int st = require_device()) return st;
+  if (bytes == 0) return PM_OK;
+  return map_err(hipMalloc(d_ptr, bytes));
+}
+
+int pm_device_free(void* d_ptr) {
+  if (!d_ptr) return PM_OK;
+  return map_err(hipFree(d_ptr));
+}
+
+int pm_copy_to_device(void* d_dst, const void* h_src, size_t bytes) {
+  if (bytes == 0) return PM_OK;
+  if (!d_dst || !h_src) return PM_ERR_INVALID;
+  if (int st = require_device()) return st;
+  return map_err(hipMemcpy(d_dst, h_src, bytes, hipMemcpyHostToDevice));
+}
+
+int pm_copy_to_host(void* h_dst, const void* d_src, size_t bytes) {
+  if (bytes == 0) return PM_OK;
+  if (!h_dst || !d_src) return PM_ERR_INVALID;
+  if (int st = require_device()) return st;
+  return map_err(hipMemcpy(h_dst, d_src, bytes, hipMemcpyDeviceToHost));
+}
+
 int pm_scene_create(const pm_mesh* meshes, int32_t num_meshes, pm_scene** out) {
   if (!out || num_meshes < 0 || (num_meshes > 0 && !meshes)) return PM_ERR_INVALID;
   *out = nullptr;

@@ -133,6 +133,10 @@ _SIGNATURES = {
     "pm_status_string": (C.c_char_p, [C.c_int]),
     "pm_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "pm_last_phase_us": (C.c_int, [C.c_int32, C.POINTER(C.c_double)]),
+    "pm_device_alloc": (C.c_int, [C.c_size_t, C.POINTER(_P)]),
+    "pm_device_free": (C.c_int, [_P]),
+    "pm_copy_to_device": (C.c_int, [_P, _P, C.c_size_t]),
+    "pm_copy_to_host": (C.c_int, [_P, _P, C.c_size_t]),
     "pm_scene_create": (C.c_int, [C.POINTER(Mesh), C.c_int32, C.POINTER(_P)]),
     "pm_scene_stats_get": (C.c_int, [_P, C.POINTER(SceneStats)]),
     "pm_scene_destroy": (C.c_int, [_P]),

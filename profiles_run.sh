@@ -7,6 +7,7 @@ OUT=$R/gpurun_out/prof
 TAG=${1:-r01}
 ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline}
 mkdir -p $OUT
+sha256sum $R/photon-mapping_amd/lib/libpm_hip.so > $OUT/lib.sha256
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o $TAG -- python3 $R/bench.py $ARGS > $OUT/${TAG}_trace_bench.log 2>&1 || exit 1

@@ -1,0 +1,114 @@
+"""The B1 process contract: the photon-mapping / photonMapping / rayTracer
+binaries (photon-mapping_amd/tools/photon_mapping_cli.cpp) driven through a
+reference-style layout: ./config.toml one level above the working directory
+(configLoader.h:6), photon text files and the PNG written to the CWD."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import conftest
+
+BIN = os.path.join(conftest.ROOT, "photon-mapping_amd", "bin")
+
+CONFIG = """[camera]
+look_from = [80.0, 30.0, 0.0]
+look_at = [10.0, 20.0, 0.0]
+look_up = [0.0, 1.0, 0.0]
+fovy = 0.87
+
+[data]
+photons_file = "global_photons.txt"
+caustics_photons_file = "caustic_photons.txt"
+model_path = "{model}"
+
+[ray-tracer]
+sky_colour = [1.0, 1.0, 1.0]
+output_filename = "result.png"
+fb_size = [{w}, {h}]
+samples_per_pixel = 1
+depth = 30
+
+[photon-mapper]
+max_depth = 10
+casted_diffuse_photons = {casted}
+casted_caustics_photons = {casted}
+"""
+
+
+def _layout(tmp_path, w=48, h=36, casted=4000):
+    (tmp_path / "config.toml").write_text(CONFIG.format(model=conftest.CORNELL, w=w, h=h, casted=casted))
+    run = tmp_path / "run"
+    run.mkdir()
+    return run
+
+
+def _run(name, cwd, *args):
+    return subprocess.run([os.path.join(BIN, name), *args], cwd=cwd, capture_output=True, text=True, timeout=600)
+
+
+def test_cli_binaries_exist():
+    for name in ("photon-mapping", "photonMapping", "rayTracer"):
+        assert os.access(os.path.join(BIN, name), os.X_OK), name
+
+
+def test_cli_missing_key_and_bad_usage(tmp_path):
+    run = _layout(tmp_path)
+    (tmp_path / "config.toml").write_text("[data]\nphotons_file = \"a.txt\"\n")
+    r = _run("photonMapping", run)
+    assert r.returncode == 1 and "missing key data.caustics_photons_file" in r.stderr
+    assert _run("photon-mapping", run, "--bogus").returncode == 2
+
+
+def test_cli_fails_loudly_without_gpu(tmp_path):
+    import pm_amd
+    if pm_amd.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    run = _layout(tmp_path)
+    r = _run("photonMapping", run)
+    assert r.returncode == 1
+    assert "no HIP device" in r.stderr
+    assert not (run / "global_photons.txt").exists()
+
+
+@pytest.mark.gpu
+def test_cli_two_stage_matches_oracle(tmp_path):
+    """photonMapping -> rayTracer: photon files byte-identical to the oracle's
+    photons written by the same %.6f writer; the PNG equals the oracle render
+    of the re-read (quantised) photons within the image tolerance."""
+    import oracle
+    import pm_amd
+    from PIL import Image
+    W, H, casted = 48, 36, 4000
+    run = _layout(tmp_path, W, H, casted)
+    r1 = _run("photonMapping", run)
+    assert r1.returncode == 0, r1.stdout + r1.stderr
+    meshes, lights = pm_amd.load_scene_file(conftest.CORNELL)
+    os_ = oracle.Scene(meshes)
+    g = oracle.trace(os_, lights, casted, 10, False)
+    c = oracle.trace(os_, lights, casted, 10, True)
+    pm_amd.write_alive_photons(g, str(tmp_path / "g_oracle.txt"))
+    pm_amd.write_alive_photons(c, str(tmp_path / "c_oracle.txt"))
+    assert (run / "global_photons.txt").read_bytes() == (tmp_path / "g_oracle.txt").read_bytes()
+    assert (run / "caustic_photons.txt").read_bytes() == (tmp_path / "c_oracle.txt").read_bytes()
+
+    r2 = _run("rayTracer", run)
+    assert r2.returncode == 0, r2.stdout + r2.stderr
+    img = np.array(Image.open(run / "result.png"))
+    assert img.shape == (H, W, 4)
+    gq = pm_amd.read_photons_from_file(str(run / "global_photons.txt"))
+    cq = pm_amd.read_photons_from_file(str(run / "caustic_photons.txt"))
+    cam = oracle.camera_setup((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
+    orgba, orgb, _ = oracle.render(os_, cam, W, H, 1, 30, (1, 1, 1), lights, oracle.PhotonMap(gq, 1.0, cq, 0.5),
+                                   oracle.PhotonMap(cq, 0.5))
+    exp = orgba.view(np.uint8).reshape(H, W, 4)
+    # make_rgba quantises to 8 bits: the 1e-3 colour tolerance allows a 1-step difference
+    assert np.abs(img.astype(int) - exp.astype(int)).max() <= 1
+    assert np.mean(np.all(img == exp, axis=2)) >= 0.999
+
+    # the one-process binary reproduces the two-process result
+    os.remove(run / "result.png")
+    r3 = _run("photon-mapping", run)
+    assert r3.returncode == 0, r3.stdout + r3.stderr
+    assert np.array_equal(np.array(Image.open(run / "result.png")), img)

@@ -4,7 +4,8 @@
 Writes:
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
   profiles/<tag>_pmc.json           per-kernel PMC totals per launch
-  profiles/pmc_gather_global.json   HBM traffic of the dominant kernel (read by bench.py)
+  profiles/pmc_gather_global.json   HBM traffic of the dominant kernel (read by bench.py only
+                                    while libpm_hip.so still has the profiled sha256)
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KiB;
 gfx950 FETCH_SIZE reports 1/2 of a wide coalesced stream's bytes, so it is
 doubled (uncalibrated for other access widths: noted in the JSON).
@@ -50,11 +51,13 @@ def main(tag="r01", src=os.path.join(ROOT, "gpurun_out", "prof"), workload=None)
         out[k] = e
     with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
-    g = [k for k in out if "k_gather<1>" in k]
+    g = [k for k in out if "k_gather<1" in k]
+    sha_file = os.path.join(src, "lib.sha256")
+    lib_sha = open(sha_file).read().split()[0] if os.path.exists(sha_file) else None
     if g and workload is not None:
         e = out[g[0]]
         with open(os.path.join(dst, "pmc_gather_global.json"), "w") as f:
-            json.dump({"kernel": g[0], "workload": workload, "tag": tag,
+            json.dump({"kernel": g[0], "workload": workload, "tag": tag, "lib_sha256": lib_sha,
                        "fetch_kib": e.get("FETCH_SIZE"), "write_kib": e.get("WRITE_SIZE"),
                        "hbm_bytes_per_launch": e.get("hbm_bytes_per_launch"),
                        "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (calibrated for wide coalesced "
