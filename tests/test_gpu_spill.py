@@ -38,8 +38,8 @@ np.savez({out!r}, hits=hits, occ=occ, ph=ph)
 
 
 def _ensure_variant():
-    if not os.path.exists(VARIANT):
-        subprocess.run(["make", "-j16", "BUILD=build_s4", "LIB=lib_s4/libpm_hip.so", "EXTRA=-DPM_STACK_DEPTH=4",
+    # incremental: rebuilds only when a source is newer than the variant
+    subprocess.run(["make", "-j16", "BUILD=build_s4", "LIB=lib_s4/libpm_hip.so", "EXTRA=-DPM_STACK_DEPTH=4",
                         "variant"], cwd=PKG, check=True, timeout=900)
 
 
