@@ -4,16 +4,17 @@
 // KNearestPhotons, ray-tracer/cuda/shading.h:11-18) and gatherPhotons
 // (shading.h:93-121). Traversal is the stack-free left-balanced kd-tree walk
 // (prev/curr with implicit parent (c+1)/2-1), so a lane needs no stack memory;
-// the candidate list is K packed u64 keys (d^2 bits << 32 | original index)
-// kept sorted in VGPRs (all indices compile-time after unrolling), so the
-// result is ordered by (d^2, index) and the radiance sum runs in that order.
+// the candidate list is K packed keys (d^2 bits << 32 | original index, held
+// as doubles: see key_make) kept sorted in VGPRs (all indices compile-time
+// after unrolling), so the result is ordered by (d^2, index) and the radiance
+// sum runs in that order.
 // Cut-off: only d^2 < max_radius^2 enters (HeapCandidateList(cutOff) init);
 // the returned radius is the K-th d^2, or max_radius^2 when fewer were found.
 //
-// The sorted 50-wide insert (~8 VALU per entry) is the dominant cost and runs
-// for the whole wave whenever any lane inserts; the production walk therefore
-// tests a node's point post-order and batches inserts wave-synchronously
-// (knn_walk<POST = true, QP = 4>; variants and measurements: DESIGN.md §4.3).
+// The sorted 50-wide insert is the dominant cost and runs for the whole wave
+// whenever any lane inserts: it is built from v_min_f64 / v_max_f64 only
+// (list_insert), and the walk tests a node's point post-order so root-path
+// points meet a tight bound (knn_walk<POST = true>; variants: DESIGN.md §4.4).
 #include <cstdio>
 #include <cstdlib>
 
@@ -21,25 +22,57 @@
 
 namespace pmd {
 
+// Candidate keys: (d^2 bits << 32 | original id) + 2^52, held as the bits of a
+// double. d^2 >= 0 so the packed integer orders candidates by (d^2, id); the
+// 2^52 bias makes every key a positive NORMAL double (exponent field >= 1,
+// never all-ones), whose IEEE order equals that integer order. The sorted
+// insert can then use the mask-free identity
+//   new[j] = max(list[j-1], min(list[j], key))
+// on v_min_f64 / v_max_f64: 99 DP ops per 50-entry insert, no compares, no
+// cndmasks, no VCC hazards (the u64 compare-select form issued ~400 slots).
+constexpr uint64_t kKeyBias = 1ull << 52;
+
+__device__ __forceinline__ double key_make(float d2, uint32_t id) {
+  return __longlong_as_double((long long)((((uint64_t)__float_as_uint(d2) << 32) | id) + kKeyBias));
+}
+__device__ __forceinline__ float key_d2(double k) {
+  return __uint_as_float((uint32_t)(((uint64_t)__double_as_longlong(k) - kKeyBias) >> 32));
+}
+__device__ __forceinline__ uint32_t key_id(double k) { return (uint32_t)__double_as_longlong(k); }
+
+// Inline asm keeps the compiler from canonicalising each operand (an extra
+// v_max_f64 x, x per op): keys are never NaN by construction.
+__device__ __forceinline__ double dmin(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double dmax(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Sorted insert of a key known to be < list[K-1] (keys are unique). Each min
+// is issued one entry ahead of the max that consumes it.
 template <int K>
-__device__ __forceinline__ void list_insert(uint64_t (&list)[K], uint64_t key) {
-  bool lt_next = true;   // key < list[K-1] checked by the caller
+__device__ __forceinline__ void list_insert(double (&list)[K], double key) {
+  double t = dmin(list[K - 1], key);
 #pragma unroll
   for (int j = K - 1; j > 0; j--) {
-    const uint64_t a = list[j - 1];
-    const bool gt = key < a;
-    list[j] = gt ? a : (lt_next ? key : list[j]);
-    lt_next = gt;
+    const double tn = dmin(list[j - 1], key);
+    list[j] = dmax(list[j - 1], t);
+    t = tn;
   }
-  list[0] = lt_next ? key : list[0];
+  list[0] = t;
 }
 
 struct KnnCounters {
   uint32_t steps = 0, ins = 0, wave_ins = 0;
 };
 
-// Stack-free walk. Production: POST = true, QP = 4 (PM_GATHER_MODE 5);
-// other instantiations are kept for A/B runs (PM_GATHER_MODE 0, 4, 6, 7).
+// Stack-free walk. Production: POST = true, QP = 0 (PM_GATHER_MODE 4); other
+// instantiations are kept for A/B runs (PM_GATHER_MODE 0, 5, 6, 7, 8).
 //  POST: a node's own point is tested when the walk comes back from its close
 //        child (or at once if it has none) instead of on arrival, so the
 //        root-path points meet an already tight bound instead of filling the
@@ -50,18 +83,18 @@ struct KnnCounters {
 //        bound ignores queued keys, i.e. it is never too tight: still exact.
 template <int K, bool POST, int QP, bool ST>
 __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n, v3 q, float r2, bool valid,
-                                         uint64_t (&list)[K], KnnCounters* kc = nullptr) {
-  const uint64_t sentinel = ((uint64_t)__float_as_uint(r2) << 32) | 0xFFFFFFFFull;
+                                         double (&list)[K], KnnCounters* kc = nullptr) {
+  const double sentinel = key_make(r2, 0xFFFFFFFFu);
 #pragma unroll
   for (int j = 0; j < K; j++) list[j] = sentinel;
   float bound = r2;
   int prev = -1, curr = 0;
   bool walking = valid && n > 0;
-  uint64_t qk[QP > 0 ? QP : 1];
+  double qk[QP > 0 ? QP : 1];
   int qn = 0;
   for (;;) {
     bool cand = false;
-    uint64_t key = 0;
+    double key = 0.0;
     if (walking) {
       const float4 nd = nodes[curr];
       const int child = 2 * curr + 1;
@@ -76,7 +109,7 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
       if (test) {
         const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
         const float d2 = dx * dx + dy * dy + dz * dz;
-        key = ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)(w >> 2);
+        key = key_make(d2, (uint32_t)(w >> 2));
         cand = d2 < r2 && key < list[K - 1];
       }
       int next;
@@ -98,7 +131,7 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
     if (QP == 0) {
       if (cand) {
         list_insert<K>(list, key);
-        bound = __uint_as_float((uint32_t)(list[K - 1] >> 32));
+        bound = key_d2(list[K - 1]);
       }
       if (ST) {
         kc->ins += cand;
@@ -116,7 +149,7 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
       // end) so the 100-VGPR list is not duplicated across the back-edge.
       const bool any_walking = __ballot(walking) != 0;
       const bool round = __ballot(qn == QP) != 0 || !any_walking;
-      uint64_t ik = ~0ull;
+      double ik = __longlong_as_double(0x7FEFFFFFFFFFFFFFll);   // DBL_MAX: never inserted
       if (round && qn > 0) {
         ik = qk[0];
 #pragma unroll
@@ -126,7 +159,7 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
       const bool ins = ik < list[K - 1];
       if (ins) {
         list_insert<K>(list, ik);
-        bound = __uint_as_float((uint32_t)(list[K - 1] >> 32));
+        bound = key_d2(list[K - 1]);
       }
       if (ST) {
         kc->ins += ins;
@@ -138,39 +171,39 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
 }
 
 template <int K, int QP>
-__global__ __launch_bounds__(256) void k_knn(const float4* nodes, int n, const pm_float3* q, int64_t nq, int k,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 64 ? 4 : 1))) void k_knn(const float4* nodes, int n, const pm_float3* q, int64_t nq, int k,
                                              float r2, int32_t* ids, float* d2o, float* maxd2) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < nq;
-  uint64_t list[K];
+  double list[K];
   const pm_float3 p = valid ? q[i] : pm_float3{0.f, 0.f, 0.f};
   knn_walk<K, true, QP, false>(nodes, n, mk(p), r2, valid, list);
   if (!valid) return;
-  uint64_t kth = list[0];
+  double kth = list[0];
 #pragma unroll
   for (int j = 0; j < K; j++) {
     if (j < k) {
-      const uint32_t id = (uint32_t)list[j];
+      const uint32_t id = key_id(list[j]);
       ids[i * k + j] = id == 0xFFFFFFFFu ? -1 : (int32_t)id;
-      if (d2o) d2o[i * k + j] = __uint_as_float((uint32_t)(list[j] >> 32));
+      if (d2o) d2o[i * k + j] = key_d2(list[j]);
     }
     if (j == k - 1) kth = list[j];
   }
-  if (maxd2) maxd2[i] = __uint_as_float((uint32_t)(kth >> 32));
+  if (maxd2) maxd2[i] = key_d2(kth);
 }
 
 // Radiance estimate from a finished candidate list: gatherPhotons
 // (shading.h:93-121), neighbours summed in (d^2, index) order.
-__device__ __forceinline__ v3 radiance(const uint64_t (&list)[kKNearest], const float4* __restrict__ payload,
+__device__ __forceinline__ v3 radiance(const double (&list)[kKNearest], const float4* __restrict__ payload,
                                        float brdf) {
-  const float r2 = __uint_as_float((uint32_t)(list[kKNearest - 1] >> 32));
+  const float r2 = key_d2(list[kKNearest - 1]);
   v3 flux = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int p = 0; p < kKNearest; p++) {
-    const uint32_t id = (uint32_t)list[p];
+    const uint32_t id = key_id(list[p]);
     if (id == 0xFFFFFFFFu) continue;
     const float4 pl = payload[id];
-    const float dist = sqrtf(__uint_as_float((uint32_t)(list[p] >> 32)));
+    const float dist = sqrtf(key_d2(list[p]));
     const float w = 1 - (dist / sqrtf(r2) * kConeFilterC);
     flux = add(flux, smul(brdf * pl.w * w, v3{pl.x, pl.y, pl.z}));
   }
@@ -179,7 +212,7 @@ __device__ __forceinline__ v3 radiance(const uint64_t (&list)[kKNearest], const 
 
 // TAG only separates the global-map launch into its own kernel symbol (rocprof).
 template <int TAG, bool POST, int QP>
-__global__ __launch_bounds__(256) void k_gather(const float4* __restrict__ nodes, const float4* __restrict__ payload,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather(const float4* __restrict__ nodes, const float4* __restrict__ payload,
                                                 int n, const float4* __restrict__ qb, int64_t nq,
                                                 float4* __restrict__ out) {
   // plain block order on purpose: consecutive blocks (Morton-adjacent queries)
@@ -188,7 +221,7 @@ __global__ __launch_bounds__(256) void k_gather(const float4* __restrict__ nodes
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < nq;
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  uint64_t list[kKNearest];
+  double list[kKNearest];
   knn_walk<kKNearest, POST, QP, false>(nodes, n, v3{qq.x, qq.y, qq.z}, kKMaxDistance * kKMaxDistance, valid, list);
   if (valid) {
     const v3 f = radiance(list, payload, qq.w);
@@ -218,7 +251,7 @@ __global__ __launch_bounds__(256) void k_gather_stats(const float4* __restrict__
   KnnCounters kc;
   const bool valid = i < nq;
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  uint64_t list[kKNearest];
+  double list[kKNearest];
   knn_walk<kKNearest, POST, QP, true>(nodes, n, v3{qq.x, qq.y, qq.z}, kKMaxDistance * kKMaxDistance, valid, list,
                                       &kc);
   const uint32_t s = wave_sum(kc.steps), in = wave_sum(kc.ins), ms = wave_max(kc.steps), wi = wave_max(kc.wave_ins);
@@ -240,7 +273,7 @@ static void gather_stats(const pm_photon_map* m, const float4* qb, int64_t nq, i
   else if (mode == 6) k_gather_stats<false, 4><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
   else if (mode == 7) k_gather_stats<true, 8><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
   else if (mode == 0) k_gather_stats<false, 0><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
-  else k_gather_stats<true, 4><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
+  else k_gather_stats<true, 0><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
   unsigned long long h[8] = {};
   if (hipMemcpyAsync(h, acc.p, 64, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
     return;
@@ -273,11 +306,11 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
     k_knn<KK, QQ><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, r2, ids, d2, maxd2);      \
     return hipGetLastError();                                                          \
   }
-  PM_KNN_CASE(8, 4)
-  PM_KNN_CASE(16, 4)
-  PM_KNN_CASE(32, 4)
-  PM_KNN_CASE(50, 4)
-  PM_KNN_CASE(64, 4)
+  PM_KNN_CASE(8, 0)
+  PM_KNN_CASE(16, 0)
+  PM_KNN_CASE(32, 0)
+  PM_KNN_CASE(50, 0)
+  PM_KNN_CASE(64, 0)
   PM_KNN_CASE(128, 0)
 #undef PM_KNN_CASE
   return hipErrorInvalidValue;
@@ -286,11 +319,13 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
 hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,
                          int tag) {
   if (nq <= 0) return hipSuccess;
-  // A/B knob (read per launch): 5 (default) post-order + 4-entry insert queue,
-  // 0 pre-order / no queue, 4 post-order / no queue, 6 pre-order + queue 4,
-  // 7 post-order + queue 8. All variants return identical bits.
+  // A/B knob (read per launch): 4 (default) post-order / no queue, 0 pre-order
+  // / no queue, 5 post-order + 4-entry insert queue, 6 pre-order + queue 4,
+  // 7 post-order + queue 8, 8 post-order + queue 3. All variants return
+  // identical bits. (With the u64 compare-select insert the queue won, 149 ->
+  // 113 ms; with the f64 min/max insert the plain post-order walk is fastest.)
   const char* env = std::getenv("PM_GATHER_MODE");
-  const int mode = env ? std::atoi(env) : 5;
+  const int mode = env ? std::atoi(env) : 4;
   if (std::getenv("PM_GATHER_STATS")) gather_stats(m, qb, nq, mode, s);
   const int g = grid_for(nq, 256);
   const int n = (int)m->n;
@@ -299,10 +334,11 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
             : (k_gather<0, P, Q><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out)))
   switch (mode) {
     case 0: PM_WALK(false, 0); break;
-    case 4: PM_WALK(true, 0); break;
+    case 5: PM_WALK(true, 4); break;
     case 6: PM_WALK(false, 4); break;
     case 7: PM_WALK(true, 8); break;
-    default: PM_WALK(true, 4); break;
+    case 8: PM_WALK(true, 3); break;
+    default: PM_WALK(true, 0); break;
   }
 #undef PM_WALK
   return hipGetLastError();
