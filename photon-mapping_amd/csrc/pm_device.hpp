@@ -267,6 +267,16 @@ __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, flo
 #define PM_STACK_DEPTH 16
 #endif
 constexpr int kStackDepth = PM_STACK_DEPTH;
+
+// Occupancy targets of the traversal kernels (waves per SIMD; 0 = compiler's
+// choice). Build-time knobs for A/B runs.
+#ifndef PM_TRACE_WAVES
+#define PM_TRACE_WAVES 6   // 6: trace 75.2 -> 69.6 ms despite 80 B/lane of spills (8: no better)
+#endif
+#ifndef PM_PATHS_WAVES
+#define PM_PATHS_WAVES 5   // 5: paths 45.5 -> 42.7 ms
+#endif
+#define PM_WAVES_ATTR(w) __attribute__((amdgpu_waves_per_eu((w) > 0 ? (w) : 1, (w) > 0 ? (w) : 10)))
 constexpr int kSpillDepth = 64 - PM_STACK_DEPTH > 0 ? 64 - PM_STACK_DEPTH : 1;
 constexpr int32_t kBvhEmpty = INT32_MIN;
 

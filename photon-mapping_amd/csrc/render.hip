@@ -179,7 +179,7 @@ struct PathOut {
   unsigned long long* rays;
 };
 
-__global__ __launch_bounds__(kRBlock) void k_paths(DevScene S, RenderArgs A, const uint32_t* voff, PathOut O,
+__global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths(DevScene S, RenderArgs A, const uint32_t* voff, PathOut O,
                                                    int* overflow) {
   __shared__ int stack[kStackDepth * kRBlock];
   const int64_t tid = (int64_t)blockIdx.x * kRBlock + threadIdx.x;
