@@ -294,6 +294,110 @@ __global__ __launch_bounds__(kPartThreads) void k_kd_part(const float4* __restri
   }
 }
 
+// ------------------------------------------------------------------ local finish
+// Once every segment holds <= kLocal - 1 elements (global level L0 = H - 10),
+// one workgroup per segment finishes all remaining levels in LDS: the three
+// presorted lists of its range are loaded once (48 KB), and each local level
+// picks every sub-segment's widest dimension and median from the lists,
+// classes the elements, runs the block-wide segmented scan and scatters in
+// place (every thread holds its three elements in registers across the
+// barrier). Same rules as the global levels, so the tree is identical; the
+// bottom ~10 levels no longer cost a global read + write each.
+constexpr int kLocal = 1024;
+
+__global__ __launch_bounds__(kLocal) void k_kd_local(const float4* __restrict__ l0, const float4* __restrict__ l1,
+                                                     const float4* __restrict__ l2, int L0, SegTab T,
+                                                     float4* __restrict__ nodes) {
+  __shared__ float4 buf[3][kLocal];
+  __shared__ int16_t tag[kLocal];
+  __shared__ int16_t sb[2][kLocal / 2], ss[2][kLocal / 2];   // sub-segment start / size, ping-pong by level
+  __shared__ int16_t sls[kLocal / 2];
+  __shared__ uint8_t sdim[kLocal / 2];
+  __shared__ float sco[kLocal / 2];
+  __shared__ int32_t sid[kLocal / 2];
+  __shared__ SegVal sh[kLocal / 64];
+  const int tid = threadIdx.x;
+  const int64_t t = ((int64_t)1 << L0) - 1 + blockIdx.x;
+  const int B = T.b[t], S = T.s[t];
+  if (S <= 0) return;
+  const float4* L[3] = {l0, l1, l2};
+  if (tid < S) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) buf[d][tid] = L[d][B + tid];
+  }
+  tag[tid] = tid < S ? 0 : -1;
+  if (tid == 0) {
+    sb[0][0] = 0;
+    ss[0][0] = (int16_t)S;
+  }
+  const int H = 32 - __clz(S);   // levels of this subtree
+  for (int k = 0; k < H; k++) {
+    const int cur = k & 1;
+    const int nsub = 1 << k;
+    __syncthreads();
+    // sub-segment roots of this level
+    if (tid < nsub) {
+      const int b = sb[cur][tid], sz = ss[cur][tid];
+      int ls = 0;
+      if (sz > 0) {
+        ls = left_size(sz);
+        float ext[3];
+#pragma unroll
+        for (int d = 0; d < 3; d++) ext[d] = coord_of(buf[d][b + sz - 1], d) - coord_of(buf[d][b], d);
+        int dim = 0;
+        if (ext[1] > ext[dim]) dim = 1;
+        if (ext[2] > ext[dim]) dim = 2;
+        const float4 e = buf[dim][b + ls];
+        const int id = __float_as_int(e.w);
+        sdim[tid] = (uint8_t)dim;
+        sco[tid] = coord_of(e, dim);
+        sid[tid] = id;
+        nodes[(t + 1) * ((int64_t)1 << k) - 1 + tid] = make_float4(e.x, e.y, e.z, __int_as_float((id << 2) | dim));
+      }
+      sls[tid] = (int16_t)ls;
+      if (k + 1 < H) {
+        const int nxt = cur ^ 1;
+        sb[nxt][2 * tid] = (int16_t)b;
+        ss[nxt][2 * tid] = (int16_t)(sz > 0 ? ls : 0);
+        sb[nxt][2 * tid + 1] = (int16_t)(b + ls + 1);
+        ss[nxt][2 * tid + 1] = (int16_t)(sz > 0 ? sz - ls - 1 : 0);
+      }
+    }
+    if (k + 1 == H) break;
+    __syncthreads();
+    // class, segmented scan and in-place stable scatter of the three lists
+    const int j = tag[tid];
+    float4 e[3];
+    uint8_t c[3];
+    SegVal th = seg_zero();
+    int b = 0, ls = 0;
+    if (j >= 0) {
+      b = sb[cur][j];
+      ls = sls[j];
+      th.f = tid == b;
+    }
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      e[d] = buf[d][tid];
+      c[d] = j < 0 ? 3 : (uint8_t)kd_class(e[d], sdim[j >= 0 ? j : 0], sco[j >= 0 ? j : 0], sid[j >= 0 ? j : 0]);
+      th.v[d] = c[d] == 0 ? 1ull : (c[d] == 2 ? (1ull << 32) : 0ull);
+    }
+    SegVal total;
+    SegVal ex = block_seg_scan<kLocal / 64>(th, sh, total);   // ends with a barrier: all reads done
+    if (th.f) ex = seg_zero();
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      int dst;
+      if (c[d] == 3) dst = tid;
+      else if (c[d] == 0) dst = b + (int)(uint32_t)ex.v[d];
+      else if (c[d] == 1) dst = b + ls;
+      else dst = b + ls + 1 + (int)(uint32_t)(ex.v[d] >> 32);
+      if (tid < S) buf[d][dst] = e[d];
+    }
+    if (j >= 0) tag[tid] = (int16_t)(tid < b + ls ? 2 * j : (tid == b + ls ? -1 : 2 * j + 1));
+  }
+}
+
 hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (n >= (1ll << 30)) return hipErrorInvalidValue;
@@ -330,7 +434,16 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
   PM_HIP_TRY(hipMemsetAsync(tag.p, 0, sizeof(int32_t) * n, s));
   float4* cur[3] = {la[0].p, la[1].p, la[2].p};
   float4* nxt[3] = {lb[0].p, lb[1].p, lb[2].p};
+  // segments at L0 hold <= 1023 elements; PM_KD_LOCAL=0 keeps every level
+  // global (A/B and the identical-tree test)
+  const char* lenv = std::getenv("PM_KD_LOCAL");
+  const int L0 = (lenv && std::atoi(lenv) == 0) ? H : std::max(0, H - 10);
   for (int L = 0; L < H; L++) {
+    if (L == L0) {
+      k_kd_local<<<(int)(1ll << L0), kLocal, 0, s>>>(cur[0], cur[1], cur[2], L0, T, nodes);
+      PM_HIP_TRY(hipGetLastError());
+      break;
+    }
     const int64_t nseg = 1ll << L;
     k_kd_seg<<<grid_for(nseg, 256), 256, 0, s>>>(cur[0], cur[1], cur[2], L, cap, T, nodes);
     PM_HIP_TRY(hipGetLastError());

@@ -172,7 +172,7 @@ hipError_t exclusive_scan_u64(const uint64_t* in, uint64_t* out, int64_t n, uint
 // 8-bit digits; tile = 256 threads x 8 rounds. Histogram -> digit-major scan
 // -> stable scatter with wave64 ballot multi-split ranking.
 constexpr int kSortBlock = 256;
-constexpr int kSortRounds = 8;
+constexpr int kSortRounds = 16;   // 4096 keys per tile: ~16 per digit run on write-out
 constexpr int kSortTile = kSortBlock * kSortRounds;
 
 __global__ __launch_bounds__(kSortBlock) void k_sort_hist(const uint32_t* keys, int64_t n, int shift,
@@ -190,23 +190,46 @@ __global__ __launch_bounds__(kSortBlock) void k_sort_hist(const uint32_t* keys, 
   hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-__global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const uint32_t* keys, const uint32_t* vals,
-                                                             uint32_t* okeys, uint32_t* ovals, int64_t n, int shift,
-                                                             const uint32_t* hoff, int nblocks) {
-  __shared__ uint32_t running[256];
+// Stable per-tile scatter: the tile is first ranked into LDS in digit order
+// (ballot multi-split per wave, rounds in input order), then written out so
+// that consecutive threads store consecutive positions of each digit's run
+// (coalesced), instead of every element landing in a different bucket line.
+__global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const uint32_t* __restrict__ keys,
+                                                             const uint32_t* __restrict__ vals,
+                                                             uint32_t* __restrict__ okeys, uint32_t* __restrict__ ovals,
+                                                             int64_t n, int shift, const uint32_t* __restrict__ hist,
+                                                             const uint32_t* __restrict__ hoff, int nblocks) {
+  __shared__ uint32_t lkey[kSortTile], lval[kSortTile];
+  __shared__ uint32_t running[256], lstart[256], gbase[256];
   __shared__ uint32_t wcnt[kSortBlock / 64][256];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  running[threadIdx.x] = hoff[(int64_t)threadIdx.x * nblocks + blockIdx.x];
+  __shared__ uint32_t wsum[kSortBlock / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // local digit starts = exclusive scan of this tile's histogram
+  const uint32_t c = hist[(int64_t)tid * nblocks + blockIdx.x];
+  uint32_t incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t up = (uint32_t)__shfl_up((int)incl, o);
+    if (lane >= o) incl += up;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t wpre = 0;
+#pragma unroll
+  for (int k = 0; k < kSortBlock / 64; k++) wpre += k < w ? wsum[k] : 0u;
+  lstart[tid] = wpre + incl - c;
+  running[tid] = wpre + incl - c;
+  gbase[tid] = hoff[(int64_t)tid * nblocks + blockIdx.x];
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
   for (int r = 0; r < kSortRounds; r++) {
 #pragma unroll
-    for (int k = 0; k < kSortBlock / 64; k++) wcnt[k][threadIdx.x] = 0;
+    for (int k = 0; k < kSortBlock / 64; k++) wcnt[k][tid] = 0;
     __syncthreads();
-    const int64_t i = base + (int64_t)r * kSortBlock + threadIdx.x;
+    const int64_t i = base + (int64_t)r * kSortBlock + tid;
     const bool valid = i < n;
-    uint32_t key = valid ? keys[i] : 0u;
-    uint32_t val = valid ? vals[i] : 0u;
+    const uint32_t key = valid ? keys[i] : 0u;
+    const uint32_t val = valid ? vals[i] : 0u;
     const uint32_t dg = (key >> shift) & 0xFF;
     uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -220,15 +243,23 @@ __global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const uint32_t* key
     if (valid) {
       uint32_t pos = running[dg] + rank;
       for (int k = 0; k < w; k++) pos += wcnt[k][dg];
-      okeys[pos] = key;
-      ovals[pos] = val;
+      lkey[pos] = key;
+      lval[pos] = val;
     }
     __syncthreads();
     uint32_t add = 0;
 #pragma unroll
-    for (int k = 0; k < kSortBlock / 64; k++) add += wcnt[k][threadIdx.x];
-    running[threadIdx.x] += add;
-    __syncthreads();
+    for (int k = 0; k < kSortBlock / 64; k++) add += wcnt[k][tid];
+    running[tid] += add;
+  }
+  __syncthreads();
+  const int tile_n = (int)min((int64_t)kSortTile, n - base);
+  for (int p = tid; p < tile_n; p += kSortBlock) {
+    const uint32_t key = lkey[p];
+    const uint32_t dg = (key >> shift) & 0xFF;
+    const uint32_t o = gbase[dg] + (uint32_t)p - lstart[dg];
+    okeys[o] = key;
+    ovals[o] = lval[p];
   }
 }
 
@@ -243,7 +274,7 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, int64_t n, int end_b
     k_sort_hist<<<nb, kSortBlock, 0, s>>>(ka, n, shift, hist.p, nb);
     PM_HIP_TRY(hipGetLastError());
     PM_HIP_TRY(exclusive_scan_u32(hist.p, hoff.p, (int64_t)256 * nb, nullptr, s));
-    k_sort_scatter<<<nb, kSortBlock, 0, s>>>(ka, va, kb, vb, n, shift, hoff.p, nb);
+    k_sort_scatter<<<nb, kSortBlock, 0, s>>>(ka, va, kb, vb, n, shift, hist.p, hoff.p, nb);
     PM_HIP_TRY(hipGetLastError());
     uint32_t* t = ka; ka = kb; kb = t;
     t = va; va = vb; vb = t;

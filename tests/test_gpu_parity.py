@@ -166,6 +166,24 @@ def test_kdtree_build_left_balanced(n):
     _check_left_balanced(out[:, :3], dims.astype(np.int64))
 
 
+@pytest.mark.parametrize("n", [5, 1023, 1024, 70000])
+def test_kdtree_local_finish_identical(n, monkeypatch):
+    """The LDS finishing kernel (bottom <= 10 levels) builds the same tree as
+    the all-global level loop."""
+    import pm_amd
+    rng = np.random.default_rng(100 + n)
+    rec = np.zeros((n, 11), np.float32)
+    rec[:, 0:3] = rng.uniform(-20, 20, size=(n, 3))
+    rec[: n // 7, 2] = 1.5          # ties on one axis
+    out = []
+    for local in ("1", "0"):
+        monkeypatch.setenv("PM_KD_LOCAL", local)
+        t = torch.from_numpy(rec.copy()).cuda()
+        pm_amd.build_tree(t)
+        out.append(t.cpu().numpy().view(np.uint32))
+    assert np.array_equal(out[0], out[1])
+
+
 def _brute_knn(pts, q, k, r):
     # same float32 evaluation order as the spec: (dx*dx + dy*dy) + dz*dz
     diff = (q[:, None, :] - pts[None, :, :]).astype(np.float32)
