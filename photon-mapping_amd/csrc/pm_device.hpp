@@ -274,7 +274,7 @@ constexpr int kStackDepth = PM_STACK_DEPTH;
 #define PM_TRACE_WAVES 6   // 6: trace 75.2 -> 69.6 ms despite 80 B/lane of spills (8: no better)
 #endif
 #ifndef PM_PATHS_WAVES
-#define PM_PATHS_WAVES 5   // 5: paths 45.5 -> 42.7 ms
+#define PM_PATHS_WAVES 0   // fused render kernel: 5 helped (45.5 -> 42.7 ms); after the ray split the default is as good
 #endif
 #define PM_WAVES_ATTR(w) __attribute__((amdgpu_waves_per_eu((w) > 0 ? (w) : 1, (w) > 0 ? (w) : 10)))
 constexpr int kSpillDepth = 64 - PM_STACK_DEPTH > 0 ? 64 - PM_STACK_DEPTH : 1;

@@ -8,9 +8,12 @@
 //                     the 20 diffuse samples is replayed (it is independent of
 //                     what the diffuse rays hit), so the path is exact.
 //   2. scan           -> deterministic vertex slots per pixel.
-//   3. k_paths        per pixel: full path with shadow rays and the 20 diffuse
-//                     rays; writes per-vertex records and one caustic + up to 20
-//                     global gather queries per vertex into fixed slots.
+//   3. k_paths        per pixel: the camera path again; writes per-vertex
+//                     records, the caustic query, and EMITS the shadow rays and
+//                     the 20 final-gather rays per vertex into fixed slots;
+//      k_diffuse_rays / k_shadow_rays trace them (lean traversal kernels at
+//                     high occupancy), k_direct sums the direct light in the
+//                     reference's order.
 //   4. compaction of valid queries, k_gather (knn.hip) per query.
 //   5. k_resolve      per pixel: replays ray_colour's colour arithmetic in the
 //                     reference's order with the gathered radiance.
@@ -175,7 +178,11 @@ struct PathOut {
   uint32_t* cvalid;
   float4* gq;         // [20 * v + j] global query (hitpoint, brdf)
   float4* galb;       // [20 * v + j] albedo of the diffuse hit
-  uint32_t* gvalid;
+  uint32_t* gvalid;   // k_paths: diffuse ray emitted; k_diffuse_rays: query valid
+  float4* gdir;       // [20 * v + j] diffuse ray direction (origin = cq[v].xyz)
+  float4* sray;       // [nl * v + l] shadow ray (direction, tmax); w < 0: not cast
+  float4* sterm;      // [nl * v + l] (ldn, inv, bs, 0) of the direct-light term
+  uint32_t* svis;     // [nl * v + l] 1 = light visible
   unsigned long long* rays;
 };
 
@@ -210,7 +217,9 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths
       } else {
         const v3 albedo = {hr.m0.x, hr.m0.y, hr.m0.z};
         const float diffuse_brdf = hr.m0.w / kPI;
-        v3 direct = {0.f, 0.f, 0.f};
+        // direct light (deviceCode.cu:145-171): the shadow rays are cast by
+        // k_shadow_rays; the per-light term is kept so that k_direct sums it
+        // in the reference's order with the visibility
         for (int l = 0; l < A.nl; l++) {
           const LightR L = A.lights[l];
           const v3 org = hr.hitpoint;
@@ -218,39 +227,33 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths
           const float dist = norm3(ldir);
           ldir = normalize(ldir);
           const float ldn = dot(ldir, hr.normal);
-          if (ldn < 0.f) continue;
-          Ray r;
-          ray_prep(r, org, ldir);
+          const int64_t si = v * A.nl + l;
+          if (ldn < 0.f) {
+            O.sray[si] = make_float4(0.f, 0.f, 0.f, -1.f);
+            continue;
+          }
           nrays++;
-          const HitInfo sh = traverse<true>(S, r, kEPS, dist * (1.f - kEPS), st, kRBlock, overflow);
-          const float vis = sh.slot >= 0 ? 0.f : 1.f;
           // specularBrdf (shading.h:82-91)
           const float sb = near_zero(sub(reflect(ldir, hr.normal), rd)) ? hr.m1.x : 0.f;
-          const float pw = L.pos.w;
           const float inv = 1.f / (dist * dist);
-          const float bs = diffuse_brdf + sb;
-          direct = add(direct, v3{vis * pw * ldn * inv * bs * L.rgb.x, vis * pw * ldn * inv * bs * L.rgb.y,
-                                  vis * pw * ldn * inv * bs * L.rgb.z});
+          O.sray[si] = make_float4(ldir.x, ldir.y, ldir.z, dist * (1.f - kEPS));
+          O.sterm[si] = make_float4(ldn, inv, diffuse_brdf + sb, 0.f);
         }
-        const v3 dt = mulv(albedo, direct);
-        O.vdirect[v] = make_float4(dt.x, dt.y, dt.z, 0.f);
         O.valb[v] = make_float4(albedo.x, albedo.y, albedo.z, 0.f);
         O.cq[v] = make_float4(hr.hitpoint.x, hr.hitpoint.y, hr.hitpoint.z, diffuse_brdf);
         O.cvalid[v] = 1;
+        // the 20 final-gather rays (deviceCode.cu:112-131): directions here (RNG
+        // order unchanged), traversal in k_diffuse_rays
         for (int j = 0; j < kNumDiffuseSamples; j++) {
           const int64_t gi = (int64_t)v * kNumDiffuseSamples + j;
-          uint32_t ok = 0;
+          uint32_t cast = 0;
           if (diffuse_brdf > 0.f) {
             const v3 rdir = diffuse_direction(hr.normal, rng);
-            HitRec dh;
+            O.gdir[gi] = make_float4(rdir.x, rdir.y, rdir.z, 0.f);
             nrays++;
-            if (trace_closest(S, hr.hitpoint, rdir, 3 * kEPS, kINFTY, dh, st, overflow) && dh.m0.w > 0.f) {
-              O.gq[gi] = make_float4(dh.hitpoint.x, dh.hitpoint.y, dh.hitpoint.z, dh.m0.w / kPI);
-              O.galb[gi] = make_float4(dh.m0.x, dh.m0.y, dh.m0.z, 0.f);
-              ok = 1;
-            }
+            cast = 1;
           }
-          O.gvalid[gi] = ok;
+          O.gvalid[gi] = cast;
         }
       }
       bool absorbed;
@@ -269,6 +272,77 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths
     }
   }
   atomicAdd(O.rays, (unsigned long long)nrays);
+}
+
+// Final-gather rays: closest hit from the vertex; a hit with a diffuse
+// material yields a global-map query (hitpoint, brdf) and its albedo
+// (closestHit + deviceCode.cu:120-129).
+__global__ __launch_bounds__(kRBlock) void k_diffuse_rays(DevScene S, const float4* __restrict__ cq,
+                                                          const float4* __restrict__ gdir, int64_t ng,
+                                                          uint32_t* __restrict__ gvalid, float4* __restrict__ gq,
+                                                          float4* __restrict__ galb, int* overflow) {
+  __shared__ int stack[kStackDepth * kRBlock];
+  const int64_t gi = (int64_t)blockIdx.x * kRBlock + threadIdx.x;
+  if (gi >= ng || !gvalid[gi]) return;
+  const float4 c = cq[gi / kNumDiffuseSamples];
+  const float4 dd = gdir[gi];
+  const v3 o = {c.x, c.y, c.z}, d = {dd.x, dd.y, dd.z};
+  Ray r;
+  ray_prep(r, o, d);
+  const HitInfo h = traverse<false>(S, r, 3 * kEPS, kINFTY, stack + threadIdx.x, kRBlock, overflow);
+  uint32_t ok = 0;
+  if (h.slot >= 0) {
+    const int mesh = __float_as_int(S.tri[3 * h.slot].w);
+    const float4 m0 = S.mat[2 * mesh];
+    if (m0.w > 0.f) {
+      const v3 hp = add(o, mulf(d, h.t));
+      gq[gi] = make_float4(hp.x, hp.y, hp.z, m0.w / kPI);
+      galb[gi] = make_float4(m0.x, m0.y, m0.z, 0.f);
+      ok = 1;
+    }
+  }
+  gvalid[gi] = ok;
+}
+
+// Shadow rays (TERMINATE_ON_FIRST_HIT): visible = no hit in (eps, dist (1 - eps)).
+__global__ __launch_bounds__(kRBlock) void k_shadow_rays(DevScene S, const float4* __restrict__ cq,
+                                                         const float4* __restrict__ sray, int nl, int64_t ns,
+                                                         uint32_t* __restrict__ svis, int* overflow) {
+  __shared__ int stack[kStackDepth * kRBlock];
+  const int64_t si = (int64_t)blockIdx.x * kRBlock + threadIdx.x;
+  if (si >= ns) return;
+  const float4 sr = sray[si];
+  if (sr.w < 0.f) return;
+  const float4 c = cq[si / nl];
+  Ray r;
+  ray_prep(r, v3{c.x, c.y, c.z}, v3{sr.x, sr.y, sr.z});
+  const HitInfo h = traverse<true>(S, r, kEPS, sr.w, stack + threadIdx.x, kRBlock, overflow);
+  svis[si] = h.slot >= 0 ? 0u : 1u;
+}
+
+// Direct light of each hit vertex, summed over the lights in order exactly as
+// deviceCode.cu:145-171 (vis * power * ldn * inv * brdf * rgb), times albedo.
+__global__ __launch_bounds__(256) void k_direct(RenderArgs A, int64_t nv, const uint32_t* __restrict__ vflags,
+                                                const float4* __restrict__ valb, const float4* __restrict__ sray,
+                                                const float4* __restrict__ sterm, const uint32_t* __restrict__ svis,
+                                                float4* __restrict__ vdirect) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= nv || (vflags[v] & VF_MISS)) return;
+  v3 direct = {0.f, 0.f, 0.f};
+  for (int l = 0; l < A.nl; l++) {
+    const int64_t si = v * A.nl + l;
+    if (sray[si].w < 0.f) continue;
+    const LightR L = A.lights[l];
+    const float4 t = sterm[si];
+    const float vis = svis[si] ? 1.f : 0.f;
+    const float pw = L.pos.w;
+    const float ldn = t.x, inv = t.y, bs = t.z;
+    direct = add(direct, v3{vis * pw * ldn * inv * bs * L.rgb.x, vis * pw * ldn * inv * bs * L.rgb.y,
+                            vis * pw * ldn * inv * bs * L.rgb.z});
+  }
+  const float4 ab = valb[v];
+  const v3 dt = mulv(v3{ab.x, ab.y, ab.z}, direct);
+  vdirect[v] = make_float4(dt.x, dt.y, dt.z, 0.f);
 }
 
 __global__ void k_compact_q(const float4* q, const uint32_t* valid, const uint32_t* idx, int64_t n, float4* dense) {
@@ -439,19 +513,35 @@ hipError_t render_impl(pm_scene* sc, const pm_render_params* P, const pm_light* 
     PM_HIP_TRY(hipStreamSynchronize(s));
   }
   const int64_t NV = V, NG = (int64_t)V * kNumDiffuseSamples;
-  DevBuf<float4> vdirect(NV), vatt(NV), valb(NV), cq(NV), gq(NG), galb(NG);
-  DevBuf<uint32_t> vflags(NV), cvalid(NV), gvalid(NG), cidx(NV), gidx(NG), ctot(1), gtot(1);
+  const int64_t NS = NV * nl;
+  DevBuf<float4> vdirect(NV), vatt(NV), valb(NV), cq(NV), gq(NG), galb(NG), gdir(NG), sray(NS), sterm(NS);
+  DevBuf<uint32_t> vflags(NV), cvalid(NV), gvalid(NG), cidx(NV), gidx(NG), ctot(1), gtot(1), svis(NS);
   DevBuf<unsigned long long> rays(1);
   if (NV > 0 && (!vdirect.p || !vatt.p || !valb.p || !cq.p || !gq.p || !galb.p || !vflags.p || !cvalid.p ||
-                 !gvalid.p || !cidx.p || !gidx.p))
+                 !gvalid.p || !cidx.p || !gidx.p || !gdir.p))
     return hipErrorOutOfMemory;
-  PathOut O{vdirect.p, vatt.p, valb.p, vflags.p, cq.p, cvalid.p, gq.p, galb.p, gvalid.p, rays.p};
+  if (NS > 0 && (!sray.p || !sterm.p || !svis.p)) return hipErrorOutOfMemory;
+  PathOut O{vdirect.p, vatt.p, valb.p, vflags.p, cq.p, cvalid.p, gq.p, galb.p, gvalid.p,
+            gdir.p, sray.p, sterm.p, svis.p, rays.p};
   uint32_t NC = 0, NGv = 0;
   {
     PhaseTimer tm(PH_PATHS, s);
     PM_HIP_TRY(hipMemsetAsync(rays.p, 0, 8, s));
     k_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, voff.p, O, sc->overflow.p);
     PM_HIP_TRY(hipGetLastError());
+    if (NG > 0) {
+      k_diffuse_rays<<<grid_for(NG, kRBlock), kRBlock, 0, s>>>(S, cq.p, gdir.p, NG, gvalid.p, gq.p, galb.p,
+                                                               sc->overflow.p);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    if (NS > 0) {
+      k_shadow_rays<<<grid_for(NS, kRBlock), kRBlock, 0, s>>>(S, cq.p, sray.p, nl, NS, svis.p, sc->overflow.p);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    if (NV > 0) {
+      k_direct<<<grid_for(NV, 256), 256, 0, s>>>(A, NV, vflags.p, valb.p, sray.p, sterm.p, svis.p, vdirect.p);
+      PM_HIP_TRY(hipGetLastError());
+    }
     PM_HIP_TRY(exclusive_scan_u32(cvalid.p, cidx.p, NV, ctot.p, s));
     PM_HIP_TRY(exclusive_scan_u32(gvalid.p, gidx.p, NG, gtot.p, s));
     PM_HIP_TRY(hipMemcpyAsync(&NC, ctot.p, 4, hipMemcpyDeviceToHost, s));
