@@ -71,8 +71,8 @@ struct KnnCounters {
   uint32_t steps = 0, ins = 0, wave_ins = 0;
 };
 
-// Stack-free walk. Production: POST = true, QP = 0 (PM_GATHER_MODE 4); other
-// instantiations are kept for A/B runs (PM_GATHER_MODE 0, 5, 6, 7, 8).
+// Stack-free walk. Production: POST = true, QL = 8 (PM_GATHER_MODE 9); other
+// instantiations are kept for A/B runs (PM_GATHER_MODE 0, 4, 5, 10).
 //  POST: a node's own point is tested when the walk comes back from its close
 //        child (or at once if it has none) instead of on arrival, so the
 //        root-path points meet an already tight bound instead of filling the
@@ -81,9 +81,12 @@ struct KnnCounters {
 //        50-wide insert round (every lane with a queued key pops one) only
 //        when some lane's queue is full or the walks are over. The pruning
 //        bound ignores queued keys, i.e. it is never too tight: still exact.
-template <int K, bool POST, int QP, bool ST>
+//  QL:   > 0 the same with a QL-deep per-lane LIFO queue in LDS (`lq`, this
+//        lane's column of a [QL][stride] array): deep batching without VGPRs.
+template <int K, bool POST, int QP, bool ST, int QL = 0>
 __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n, v3 q, float r2, bool valid,
-                                         double (&list)[K], KnnCounters* kc = nullptr) {
+                                         double (&list)[K], KnnCounters* kc = nullptr, double* lq = nullptr,
+                                         int lstride = 0) {
   const double sentinel = key_make(r2, 0xFFFFFFFFu);
 #pragma unroll
   for (int j = 0; j < K; j++) list[j] = sentinel;
@@ -128,7 +131,29 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
       }
       if (ST) kc->steps++;
     }
-    if (QP == 0) {
+    if (QL > 0) {
+      if (cand) {
+        lq[qn * lstride] = key;
+        qn++;
+      }
+      const bool any_walking = __ballot(walking) != 0;
+      const bool round = __ballot(qn == QL) != 0 || !any_walking;
+      double ik = __longlong_as_double(0x7FEFFFFFFFFFFFFFll);   // DBL_MAX: never inserted
+      if (round && qn > 0) {
+        qn--;
+        ik = lq[qn * lstride];
+      }
+      const bool ins = ik < list[K - 1];
+      if (ins) {
+        list_insert<K>(list, ik);
+        bound = key_d2(list[K - 1]);
+      }
+      if (ST) {
+        kc->ins += ins;
+        kc->wave_ins += round;
+      }
+      if (!any_walking && __ballot(qn > 0) == 0) break;
+    } else if (QP == 0) {
       if (cand) {
         list_insert<K>(list, key);
         bound = key_d2(list[K - 1]);
@@ -211,10 +236,11 @@ __device__ __forceinline__ v3 radiance(const double (&list)[kKNearest], const fl
 }
 
 // TAG only separates the global-map launch into its own kernel symbol (rocprof).
-template <int TAG, bool POST, int QP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather(const float4* __restrict__ nodes, const float4* __restrict__ payload,
-                                                int n, const float4* __restrict__ qb, int64_t nq,
-                                                float4* __restrict__ out) {
+template <int TAG, bool POST, int QP, int QL = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather(
+    const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
+    int64_t nq, float4* __restrict__ out) {
+  __shared__ double lq[QL > 0 ? QL * 256 : 1];
   // plain block order on purpose: consecutive blocks (Morton-adjacent queries)
   // spread over the 8 XCDs keep ONE narrow window of the tree live in the
   // shared Infinity Cache; an XCD-contiguous remap measured 9 % slower.
@@ -222,7 +248,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool valid = i < nq;
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   double list[kKNearest];
-  knn_walk<kKNearest, POST, QP, false>(nodes, n, v3{qq.x, qq.y, qq.z}, kKMaxDistance * kKMaxDistance, valid, list);
+  knn_walk<kKNearest, POST, QP, false, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, kKMaxDistance * kKMaxDistance, valid,
+                                           list, nullptr, lq + threadIdx.x, 256);
   if (valid) {
     const v3 f = radiance(list, payload, qq.w);
     out[i] = make_float4(f.x, f.y, f.z, 0.f);
@@ -243,7 +270,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-template <bool POST, int QP>
+template <bool POST, int QP, int QL = 0>
 __global__ __launch_bounds__(256) void k_gather_stats(const float4* __restrict__ nodes, int n,
                                                       const float4* __restrict__ qb, int64_t nq,
                                                       unsigned long long* acc) {
@@ -252,8 +279,9 @@ __global__ __launch_bounds__(256) void k_gather_stats(const float4* __restrict__
   const bool valid = i < nq;
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   double list[kKNearest];
-  knn_walk<kKNearest, POST, QP, true>(nodes, n, v3{qq.x, qq.y, qq.z}, kKMaxDistance * kKMaxDistance, valid, list,
-                                      &kc);
+  __shared__ double lq[QL > 0 ? QL * 256 : 1];
+  knn_walk<kKNearest, POST, QP, true, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, kKMaxDistance * kKMaxDistance, valid,
+                                          list, &kc, lq + threadIdx.x, 256);
   const uint32_t s = wave_sum(kc.steps), in = wave_sum(kc.ins), ms = wave_max(kc.steps), wi = wave_max(kc.wave_ins);
   if ((threadIdx.x & 63) == 0) {
     atomicAdd(&acc[0], (unsigned long long)s);
@@ -270,10 +298,9 @@ static void gather_stats(const pm_photon_map* m, const float4* qb, int64_t nq, i
   const int g = grid_for(nq, 256);
   if (mode == 4) k_gather_stats<true, 0><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
   else if (mode == 5) k_gather_stats<true, 4><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
-  else if (mode == 6) k_gather_stats<false, 4><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
-  else if (mode == 7) k_gather_stats<true, 8><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
   else if (mode == 0) k_gather_stats<false, 0><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
-  else k_gather_stats<true, 0><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
+  else if (mode == 10) k_gather_stats<true, 0, 16><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
+  else k_gather_stats<true, 0, 8><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
   unsigned long long h[8] = {};
   if (hipMemcpyAsync(h, acc.p, 64, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
     return;
@@ -319,26 +346,27 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
 hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,
                          int tag) {
   if (nq <= 0) return hipSuccess;
-  // A/B knob (read per launch): 4 (default) post-order / no queue, 0 pre-order
-  // / no queue, 5 post-order + 4-entry insert queue, 6 pre-order + queue 4,
-  // 7 post-order + queue 8, 8 post-order + queue 3. All variants return
-  // identical bits. (With the u64 compare-select insert the queue won, 149 ->
-  // 113 ms; with the f64 min/max insert the plain post-order walk is fastest.)
+  // A/B knob (read per launch), all variants return identical bits:
+  //   9 (default) post-order + 8-deep LDS insert queue        66.3 ms
+  //   4 post-order, insert at once                             73.6 ms
+  //   5 post-order + 4-entry VGPR queue (spills)               74.1 ms
+  //  10 post-order + 16-deep LDS queue (staler bound)          69.1 ms
+  //   0 pre-order, insert at once
+  // (config 3 global map; depths 4 / 6: 67.3 / 66.4 ms)
   const char* env = std::getenv("PM_GATHER_MODE");
-  const int mode = env ? std::atoi(env) : 4;
+  const int mode = env ? std::atoi(env) : 9;
   if (std::getenv("PM_GATHER_STATS")) gather_stats(m, qb, nq, mode, s);
   const int g = grid_for(nq, 256);
   const int n = (int)m->n;
-#define PM_WALK(P, Q)                                                                                   \
-  (tag == 1 ? (k_gather<1, P, Q><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out))             \
-            : (k_gather<0, P, Q><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out)))
+#define PM_WALK(P, Q, L)                                                                                \
+  (tag == 1 ? (k_gather<1, P, Q, L><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out))          \
+            : (k_gather<0, P, Q, L><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out)))
   switch (mode) {
-    case 0: PM_WALK(false, 0); break;
-    case 5: PM_WALK(true, 4); break;
-    case 6: PM_WALK(false, 4); break;
-    case 7: PM_WALK(true, 8); break;
-    case 8: PM_WALK(true, 3); break;
-    default: PM_WALK(true, 0); break;
+    case 0: PM_WALK(false, 0, 0); break;
+    case 4: PM_WALK(true, 0, 0); break;
+    case 5: PM_WALK(true, 4, 0); break;
+    case 10: PM_WALK(true, 0, 16); break;
+    default: PM_WALK(true, 0, 8); break;
   }
 #undef PM_WALK
   return hipGetLastError();
