@@ -2,8 +2,11 @@
 //
 // Replaces common/src/configLoader.h:8-19 (toml11 4.2.0 `toml::parse` of the
 // fixed path "../config.toml") with a TOML-subset parser covering exactly what
-// the reference reads: tables, bare/quoted keys, basic strings, integers
-// (with '_' separators, config.toml.example:26), floats, booleans, arrays.
+// the reference reads: tables, bare/quoted/dotted keys, basic and literal
+// strings (all basic escapes), integers (decimal with '_' separators,
+// config.toml.example:26, and 0x/0o/0b), floats (incl. inf/nan), booleans,
+// arrays. Cross-checked against the reference's own toml11 (oracle/ref,
+// tests/test_toml_ref.py).
 // Type rules follow toml11's accessors used by the reference: `as_integer()`
 // rejects floats and `as_floating()` rejects integers (configLoader.h:21-29),
 // so `fovy = 1` or `look_at = [1, 2, 3]` is an error, as it is upstream.
@@ -57,7 +60,7 @@ struct Parser {
       }
     }
   }
-  bool parse_key(std::string& k) {
+  bool parse_key_part(std::string& k) {
     skip_ws();
     k.clear();
     if (p < src.size() && (src[p] == '"' || src[p] == '\'')) {
@@ -70,6 +73,35 @@ struct Parser {
     if (k.empty()) return fail("expected key");
     return true;
   }
+  // dotted keys (a.b = v, [a.b]) flatten to "a.b"
+  bool parse_key(std::string& k) {
+    if (!parse_key_part(k)) return false;
+    for (;;) {
+      skip_ws();
+      if (p >= src.size() || src[p] != '.') return true;
+      p++;
+      std::string part;
+      if (!parse_key_part(part)) return false;
+      k += "." + part;
+    }
+  }
+  static void utf8(std::string& out, unsigned long cp) {
+    if (cp < 0x80) {
+      out += (char)cp;
+    } else if (cp < 0x800) {
+      out += (char)(0xC0 | (cp >> 6));
+      out += (char)(0x80 | (cp & 0x3F));
+    } else if (cp < 0x10000) {
+      out += (char)(0xE0 | (cp >> 12));
+      out += (char)(0x80 | ((cp >> 6) & 0x3F));
+      out += (char)(0x80 | (cp & 0x3F));
+    } else {
+      out += (char)(0xF0 | (cp >> 18));
+      out += (char)(0x80 | ((cp >> 12) & 0x3F));
+      out += (char)(0x80 | ((cp >> 6) & 0x3F));
+      out += (char)(0x80 | (cp & 0x3F));
+    }
+  }
   bool parse_string(TVal& v) {
     char q = src[p++];
     v.kind = TVal::STR;
@@ -81,9 +113,23 @@ struct Parser {
         switch (e) {
           case 'n': v.s += '\n'; break;
           case 't': v.s += '\t'; break;
+          case 'b': v.s += '\b'; break;
+          case 'f': v.s += '\f'; break;
+          case 'r': v.s += '\r'; break;
           case '\\': v.s += '\\'; break;
           case '"': v.s += '"'; break;
-          default: v.s += e; break;
+          case 'u':
+          case 'U': {
+            const size_t nd = e == 'u' ? 4 : 8;
+            if (p + nd > src.size()) return fail("bad unicode escape");
+            const std::string hex = src.substr(p, nd);
+            for (char h : hex)
+              if (!std::isxdigit((unsigned char)h)) return fail("bad unicode escape");
+            utf8(v.s, std::strtoul(hex.c_str(), nullptr, 16));
+            p += nd;
+            break;
+          }
+          default: return fail(std::string("bad escape \\") + e);
         }
         continue;
       }
@@ -104,15 +150,28 @@ struct Parser {
       v.b = t == "true";
       return true;
     }
-    for (size_t i = 0; i < t.size(); i++) {
+    // 0x / 0o / 0b integers (no sign), underscores between digits
+    int radix = 10;
+    if (t.size() > 2 && t[0] == '0' && (t[1] == 'x' || t[1] == 'o' || t[1] == 'b')) radix = t[1] == 'x' ? 16 : (t[1] == 'o' ? 8 : 2);
+    auto is_digit = [&](char ch) { return radix == 16 ? std::isxdigit((unsigned char)ch) != 0 : std::isdigit((unsigned char)ch) != 0; };
+    for (size_t i = radix == 10 ? 0 : 2; i < t.size(); i++) {
       if (t[i] == '_') {
         // TOML: underscores only between digits
-        if (i == 0 || i + 1 >= t.size() || !std::isdigit((unsigned char)t[i - 1]) ||
-            !std::isdigit((unsigned char)t[i + 1]))
+        if (i == 0 || i + 1 >= t.size() || !is_digit(t[i - 1]) || !is_digit(t[i + 1]))
           return fail("bad underscore in number '" + t + "'");
         continue;
       }
       c += t[i];
+    }
+    if (radix != 10) {
+      char* e2 = nullptr;
+      if (c.empty()) return fail("bad number '" + t + "'");
+      for (char ch : c)
+        if (!(radix == 16 ? std::isxdigit((unsigned char)ch) : (ch >= '0' && ch < '0' + radix)))
+          return fail("bad number '" + t + "'");
+      v.kind = TVal::INT;
+      v.i = (long long)std::strtoull(c.c_str(), &e2, radix);
+      return true;
     }
     if (c.empty()) return fail("expected value");
     std::string body = (c[0] == '+' || c[0] == '-') ? c.substr(1) : c;
