@@ -64,8 +64,15 @@ typedef struct {
   pm_material material;
 } pm_mesh;
 
-/* common/src/world.h:11-27 (LightSource, 64 B). Only POINT_LIGHT is traced,
- * as in the reference (assetImporter.cxx:122). */
+/* common/src/world.h:11-27 (LightSource, 64 B). POINT_LIGHT is the
+ * reference's emitter (pointLightRayGen). SQUARE_LIGHT is declared by the
+ * reference but never emitted there; this build defines it: the photon origin
+ * is uniform on the side_length square centred at pos, perpendicular to
+ * normal (basis t1 = normalize(cross(a, n)), t2 = cross(n, t1), a = (0,1,0) if
+ * |n.x| > 0.9 else (1,0,0); two RNG draws), the direction a cosine lobe about
+ * normal. lights.txt lines with 11 values "x y z r g b power nx ny nz side"
+ * load as SQUARE_LIGHT. The final-gather render lights every source as a point
+ * at pos, as the reference's direct-light loop does. */
 enum { PM_POINT_LIGHT = 0, PM_SQUARE_LIGHT = 1 };
 typedef struct {
   int32_t source_type;

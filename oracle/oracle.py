@@ -75,6 +75,7 @@ def _load():
         "orc_sinf": (C.c_float, [C.c_float]),
         "orc_cosf": (C.c_float, [C.c_float]),
         "orc_random_point_in_unit_sphere": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_float)]),
+        "orc_emit_photon": (None, [C.POINTER(Light), C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
         "orc_refract": (None, [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_float, C.POINTER(C.c_float)]),
         "orc_scene_create": (C.c_int, [C.POINTER(Mesh), C.c_int32, C.c_int32, C.POINTER(_P)]),
         "orc_scene_destroy": (None, [_P]),
@@ -120,6 +121,10 @@ def lights_array(lights):
         arr[i].pos = _f3(l["pos"])
         arr[i].rgb = _f3(l["rgb"])
         arr[i].power = float(l["power"])
+        if "side" in l:   # SQUARE_LIGHT
+            arr[i].source_type = 1
+            arr[i].normal = _f3(l["normal"])
+            arr[i].side_length = float(l["side"])
     return arr
 
 
@@ -162,6 +167,14 @@ class Scene:
         if getattr(self, "h", None):
             lib.orc_scene_destroy(self.h)
             self.h = None
+
+
+def emit_photon(light: dict, pid: int):
+    """(origin, direction) of photon `pid` of one light (RNG seeded (pid, 0))."""
+    arr = lights_array([light])
+    o, d = (C.c_float * 3)(), (C.c_float * 3)()
+    lib.orc_emit_photon(arr, pid, o, d)
+    return np.array(o[:], np.float32), np.array(d[:], np.float32)
 
 
 def photons_per_light(lights, casted):

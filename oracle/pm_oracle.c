@@ -525,6 +525,36 @@ typedef struct {
 
 /* photon-mapping/cuda/deviceCode.cu:54-72 (raygen) + :25-52 (bounce loops)
  * + :113-131 (closest hit) + :74-111 (scatter) + :10-17 (deposit). */
+/* Emission: point light = pointLightRayGen (deviceCode.cu:54-72); SQUARE_LIGHT
+ * = this build's definition (the reference declares the type only, world.h:
+ * 8-24): origin uniform on the side x side square about pos in the basis
+ * t1 = normalize(cross(a, n)), t2 = cross(n, t1), a = (0,1,0) if |n.x| > 0.9
+ * else (1,0,0) (two draws), direction = cosine lobe about n. */
+static void emit_photon(const pm_light* L, uint32_t* rng, v3* o, v3* d) {
+  if (L->source_type == PM_SQUARE_LIGHT) {
+    const v3 n = normalize(fromp(L->normal));
+    const v3 a = fabsf(n.x) > 0.9f ? V3(0.f, 1.f, 0.f) : V3(1.f, 0.f, 0.f);
+    const v3 t1 = normalize(cross(a, n));
+    const v3 t2 = cross(n, t1);
+    const float side = (float)L->side_length;
+    const float u = orc_lcg_next(rng);
+    const float w = orc_lcg_next(rng);
+    *o = add(add(fromp(L->pos), smul((u - 0.5f) * side, t1)), smul((w - 0.5f) * side, t2));
+    *d = cosine_sample_hemisphere(n, rng);
+  } else {
+    *o = fromp(L->pos);
+    *d = random_point_in_unit_sphere(rng);
+  }
+}
+
+void orc_emit_photon(const pm_light* L, uint32_t id, float o[3], float d[3]) {
+  uint32_t rng = orc_lcg_init(id, 0);
+  v3 oo, dd;
+  emit_photon(L, &rng, &oo, &dd);
+  o[0] = oo.x; o[1] = oo.y; o[2] = oo.z;
+  d[0] = dd.x; d[1] = dd.y; d[2] = dd.z;
+}
+
 static void trace_one(const trace_ctx* c, int64_t g) {
   int l = 0;
   while (g >= c->loff[l + 1]) l++;
@@ -532,8 +562,8 @@ static void trace_one(const trace_ctx* c, int64_t g) {
   const pm_light* L = &c->lights[l];
   uint32_t rng = orc_lcg_init(id, 0);
   v3 color = fromp(L->rgb);
-  v3 o = fromp(L->pos);
-  v3 d = random_point_in_unit_sphere(&rng);
+  v3 o, d;
+  emit_photon(L, &rng, &o, &d);
   const float tmin = EPS;
   pm_photon* out = &c->slots[(g - c->g_lo) * c->maxd];
   int n = 0;

@@ -26,6 +26,9 @@ extern "C" {
 #endif
 
 typedef struct orc_scene orc_scene;
+
+/* Photon id's emission (origin, direction) of one light, RNG seeded (id, 0). */
+void orc_emit_photon(const pm_light* light, uint32_t id, float o[3], float d[3]);
 typedef struct orc_map orc_map;
 
 /* --- scalar kernels exposed for known-answer tests --- */

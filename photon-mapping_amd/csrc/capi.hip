@@ -23,10 +23,6 @@ namespace pmd {
 
 hipError_t launch_query(pm_scene* sc, const pm_ray* rays, int64_t n, pm_hit* hits, int32_t* occ, bool any,
                         hipStream_t s);
-struct LightDev {
-  float4 pos;
-  float4 rgb;
-};
 hipError_t launch_trace_chunk(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl, int64_t g_lo,
                               int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt, hipStream_t s);
 hipError_t launch_compact(const pm_photon* slots, const uint32_t* cnt, const uint32_t* off, int64_t np,
@@ -329,7 +325,10 @@ int pm_trace_photons(pm_scene* sc, const pm_light* lights, int32_t nl, const pm_
   std::vector<LightDev> lh(nl);
   for (int i = 0; i < nl; i++) {
     lh[i].pos = make_float4(lights[i].pos.x, lights[i].pos.y, lights[i].pos.z, 0.f);
-    lh[i].rgb = make_float4(lights[i].rgb.x, lights[i].rgb.y, lights[i].rgb.z, 0.f);
+    lh[i].rgb = make_float4(lights[i].rgb.x, lights[i].rgb.y, lights[i].rgb.z,
+                            lights[i].source_type == PM_SQUARE_LIGHT ? 1.f : 0.f);
+    lh[i].nrm = make_float4(lights[i].normal.x, lights[i].normal.y, lights[i].normal.z,
+                            (float)lights[i].side_length);
   }
   DevBuf<LightDev> dl(nl);
   DevBuf<int64_t> dloff(nl + 1);

@@ -9,7 +9,9 @@
 //   * extract_objects (assetImporter.cxx:33-96): BFS over nodes, transform =
 //     node * parent (:43), per-mesh vertex de-duplication by exact position in
 //     first-occurrence order (:65-73), mesh name = material name (:87-90);
-//   * extract_lights (:98-134): <dir>/lights.txt, "x y z r g b power";
+//   * extract_lights (:98-134): <dir>/lights.txt, "x y z r g b power"; a line
+//     "x y z r g b power nx ny nz side" is a SQUARE_LIGHT (this build's
+//     extension);
 //   * assign_materials (:139-205): <stem>.mtl, "name r g b d s t ior",
 //     default white diffuse with ior 0.
 // Deviation: the reference rewrites '/' to '\\' before
@@ -23,6 +25,7 @@
 #include <fstream>
 #include <map>
 #include <memory>
+#include <iterator>
 #include <sstream>
 #include <string>
 #include <unordered_map>
@@ -529,6 +532,18 @@ extern "C" int pm_scene_data_load(const char* cpath, pm_scene_data** out) {
       if (!(is >> L.pos.x >> L.pos.y >> L.pos.z >> L.rgb.x >> L.rgb.y >> L.rgb.z >> L.power)) {
         std::fprintf(stderr, "pm: Invalid light source data format\n");
         return PM_ERR_IO;
+      }
+      // extension (this build): "... power nx ny nz side" = SQUARE_LIGHT
+      std::string extra;
+      if (is >> extra) {
+        std::istringstream rest(extra + " " + std::string(std::istreambuf_iterator<char>(is), {}));
+        double side = 0;
+        if (!(rest >> L.normal.x >> L.normal.y >> L.normal.z >> side)) {
+          std::fprintf(stderr, "pm: Invalid light source data format\n");
+          return PM_ERR_IO;
+        }
+        L.source_type = PM_SQUARE_LIGHT;
+        L.side_length = side;
       }
       S->lights.push_back(L);
     }

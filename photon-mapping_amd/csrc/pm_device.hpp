@@ -385,6 +385,31 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
   return h;
 }
 
+// Photon emission. Point light: pointLightRayGen (photon-mapping/cuda/
+// deviceCode.cu:54-72), origin = light position, direction =
+// randomPointInUnitSphere. SQUARE_LIGHT (declared by the reference, world.h:
+// 8-24, never emitted there; this build's definition): two draws place the
+// origin uniformly on the side x side square centred at pos, spanned by
+// t1 = normalize(cross(a, n)), t2 = cross(n, t1) with a = (0,1,0) if |n.x| >
+// 0.9 else (1,0,0); the direction is the cosine lobe about n used by diffuse
+// scattering. The oracle restates the same operations in the same order.
+__device__ __forceinline__ void emit_photon(float type, v3 pos, v3 normal, float side, uint32_t& rng, v3& o,
+                                            v3& d) {
+  if (type == 1.0f) {
+    const v3 n = normalize(normal);
+    const v3 a = fabsf(n.x) > 0.9f ? v3{0.f, 1.f, 0.f} : v3{1.f, 0.f, 0.f};
+    const v3 t1 = normalize(cross(a, n));
+    const v3 t2 = cross(n, t1);
+    const float u = lcg_next(rng);
+    const float w = lcg_next(rng);
+    o = add(add(pos, smul((u - 0.5f) * side, t1)), smul((w - 0.5f) * side, t2));
+    d = cosine_sample_hemisphere(n, rng);
+  } else {
+    o = pos;
+    d = random_point_in_unit_sphere(rng);
+  }
+}
+
 __device__ __forceinline__ v3 tri_normal(const DevScene& S, int slot) {
   const float4 a = S.tri[3 * slot + 0];
   const float4 b = S.tri[3 * slot + 1];

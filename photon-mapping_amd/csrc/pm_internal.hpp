@@ -40,6 +40,14 @@ struct pm_photon_map {
 
 namespace pmd {
 
+// Light for the photon tracer: pos.xyz, rgb.xyz, rgb.w = type (0 point,
+// 1 square), nrm = (normal.xyz, side length).
+struct LightDev {
+  float4 pos;
+  float4 rgb;
+  float4 nrm;
+};
+
 // phase timers (pm_last_phase_us)
 enum Phase { PH_TRACE = 0, PH_COMPACT = 1, PH_KDBUILD = 2, PH_PATHS = 3, PH_GATHER = 4, PH_RESOLVE = 5, PH_BVH = 6,
              PH_GATHER_GLOBAL = 7, PH_COUNT = 8 };

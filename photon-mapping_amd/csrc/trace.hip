@@ -19,11 +19,6 @@ namespace pmd {
 
 constexpr int kTBlock = 128;
 
-struct LightDev {
-  float4 pos;   // xyz
-  float4 rgb;   // xyz
-};
-
 // Each lane traces several photons back to back (i, i + stride, ...): when a
 // photon's path ends the lane immediately starts its next photon, so a wave
 // is not held by its longest path (path lengths range over 1..max_depth).
@@ -53,8 +48,7 @@ __global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TRACE_WAVES) void k_trace
       const LightDev L = lights[l];
       rng = lcg_init(id, 0u);
       color = {L.rgb.x, L.rgb.y, L.rgb.z};
-      o = {L.pos.x, L.pos.y, L.pos.z};
-      d = random_point_in_unit_sphere(rng);
+      emit_photon(L.rgb.w, v3{L.pos.x, L.pos.y, L.pos.z}, v3{L.nrm.x, L.nrm.y, L.nrm.z}, L.nrm.w, rng, o, d);
       n = 0;
       b = 0;
       alive = true;
@@ -143,9 +137,10 @@ __global__ __launch_bounds__(256) void k_ph_gen(const LightDev* __restrict__ lig
   const uint32_t id = (uint32_t)(g - loff[l]);
   const LightDev L = lights[l];
   uint32_t rng = lcg_init(id, 0u);
-  const v3 d = random_point_in_unit_sphere(rng);
+  v3 o, d;
+  emit_photon(L.rgb.w, v3{L.pos.x, L.pos.y, L.pos.z}, v3{L.nrm.x, L.nrm.y, L.nrm.z}, L.nrm.w, rng, o, d);
   PhotonRay r;
-  r.o = make_float4(L.pos.x, L.pos.y, L.pos.z, __uint_as_float(rng));
+  r.o = make_float4(o.x, o.y, o.z, __uint_as_float(rng));
   r.d = make_float4(d.x, d.y, d.z, __uint_as_float((uint32_t)i));
   r.c = make_float4(L.rgb.x, L.rgb.y, L.rgb.z, __uint_as_float(0u));
   rays[i] = r;

@@ -238,18 +238,31 @@ class MeshData:
 
 
 def lights_array(lights: Sequence[dict]) -> C.Array:
+    """LightSource (world.h:13-24) array. A dict with "normal" and "side" is a
+    SQUARE_LIGHT (this build's emission definition, include/pm.h)."""
     arr = (Light * max(1, len(lights)))()
     for i, l in enumerate(lights):
-        arr[i].source_type = 0
+        square = "side" in l
+        arr[i].source_type = 1 if square else 0
         arr[i].pos = _f3(l["pos"])
         arr[i].rgb = _f3(l["rgb"])
         arr[i].power = float(l["power"])
+        if square:
+            arr[i].normal = _f3(l["normal"])
+            arr[i].side_length = float(l["side"])
     return arr
 
 
 def light_dicts(arr, n: int) -> List[dict]:
-    return [{"pos": (arr[i].pos.x, arr[i].pos.y, arr[i].pos.z), "rgb": (arr[i].rgb.x, arr[i].rgb.y, arr[i].rgb.z),
-             "power": arr[i].power} for i in range(n)]
+    out = []
+    for i in range(n):
+        d = {"pos": (arr[i].pos.x, arr[i].pos.y, arr[i].pos.z), "rgb": (arr[i].rgb.x, arr[i].rgb.y, arr[i].rgb.z),
+             "power": arr[i].power}
+        if arr[i].source_type == 1:
+            d["normal"] = (arr[i].normal.x, arr[i].normal.y, arr[i].normal.z)
+            d["side"] = arr[i].side_length
+        out.append(d)
+    return out
 
 
 def load_scene_file(path: str):

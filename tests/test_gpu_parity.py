@@ -91,6 +91,21 @@ def test_trace_bitwise(which, casted, caustics, request):
     assert len(pg) > 0
 
 
+@pytest.mark.parametrize("caustics", [False, True])
+def test_trace_square_light_bitwise(cornell, caustics):
+    """SQUARE_LIGHT emission (this build's definition) traced bit-identically."""
+    import oracle
+    import pm_amd
+    meshes, _ = cornell
+    lights = [dict(pos=(0.0, 39.0, 0.0), rgb=(1.0, 0.9, 0.8), power=30.0, normal=(0.0, -1.0, 0.0), side=8.0),
+              dict(pos=(-10.0, 20.0, 5.0), rgb=(1.0, 1.0, 1.0), power=10.0, normal=(1.0, 0.2, 0.0), side=3.0),
+              dict(pos=(5.0, 30.0, -5.0), rgb=(0.5, 0.5, 1.0), power=10.0)]
+    gs, os_ = _scene_pair(meshes)
+    pg = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, caustics).cpu().numpy()
+    po = oracle.trace(os_, lights, 30000, 10, caustics)
+    assert len(pg) > 0 and np.array_equal(_bits(pg), _bits(po))
+
+
 def test_trace_shards_concatenate(cornell):
     import pm_amd
     meshes, lights = cornell

@@ -140,6 +140,23 @@ def test_ingest_fallbacks(tmp_path, capfd):
         pm_amd.load_scene_file(str(tmp_path / "box.glb"))
 
 
+def test_square_light_line(tmp_path):
+    """lights.txt extension of this build: 11 values = SQUARE_LIGHT (normal,
+    side); 7 = point light as in the reference; anything in between is an
+    invalid line (the reference's runtime_error)."""
+    import pm_amd
+    src = os.path.join(conftest.SCENES, "cornell-box")
+    shutil.copy(os.path.join(src, "cornell-box.glb"), tmp_path / "box.glb")
+    (tmp_path / "lights.txt").write_text("0 39 0 1 0.9 0.8 100 0 -1 0 5\n1 2 3 1 1 1 5.5\n")
+    _, lights = pm_amd.load_scene_file(str(tmp_path / "box.glb"))
+    assert lights[0] == {"pos": (0.0, 39.0, 0.0), "rgb": (1.0, pytest.approx(0.9), pytest.approx(0.8)),
+                         "power": 100.0, "normal": (0.0, -1.0, 0.0), "side": 5.0}
+    assert lights[1] == {"pos": (1.0, 2.0, 3.0), "rgb": (1.0, 1.0, 1.0), "power": 5.5}
+    (tmp_path / "lights.txt").write_text("0 39 0 1 1 1 100 0 -1\n")
+    with pytest.raises(pm_amd.PMError):
+        pm_amd.load_scene_file(str(tmp_path / "box.glb"))
+
+
 def test_obj_ingest(tmp_path):
     import pm_amd
     (tmp_path / "lights.txt").write_text("0 5 0 1 1 1 10\n")

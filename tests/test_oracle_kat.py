@@ -275,3 +275,40 @@ def test_oracle_render_invariants(cornell):
     parts = [oracle.render(s, cam, 40, 30, 1, 30, (1, 1, 1), lights, gm, cm, tile_rank=r, tile_count=3)[0]
              for r in range(3)]
     assert np.array_equal(parts[0] | parts[1] | parts[2], full)
+
+
+def test_square_light_emission():
+    """SQUARE_LIGHT (this build's definition, pm_device.hpp emit_photon): origin
+    uniform on the square about pos in the plane normal to n, direction in the
+    hemisphere of n (cosine lobe); a point light keeps pointLightRayGen."""
+    import oracle
+    n = np.array([0.3, -1.0, 0.2], np.float32)
+    n /= np.linalg.norm(n)
+    L = dict(pos=(1.0, 10.0, -2.0), rgb=(1, 1, 1), power=50.0, normal=tuple(n), side=4.0)
+    pts, dirs = [], []
+    for pid in range(4000):
+        o, d = oracle.emit_photon(L, pid)
+        pts.append(o)
+        dirs.append(d)
+    pts, dirs = np.array(pts), np.array(dirs)
+    rel = pts - np.array(L["pos"], np.float32)
+    assert np.abs(rel @ n).max() < 1e-5                               # in the light's plane
+    a = np.array([0, 1, 0] if abs(n[0]) > 0.9 else [1, 0, 0], np.float32)
+    t1 = np.cross(a, n)
+    t1 /= np.linalg.norm(t1)
+    t2 = np.cross(n, t1)
+    u, v = rel @ t1, rel @ t2
+    assert np.abs(u).max() <= 2.0 + 1e-5 and np.abs(v).max() <= 2.0 + 1e-5
+    assert abs(u.mean()) < 0.1 and abs(v.mean()) < 0.1 and u.std() > 1.0   # ~uniform on [-2, 2]
+    cos = dirs @ n
+    assert cos.min() > 0 and abs(np.linalg.norm(dirs, axis=1) - 1).max() < 1e-5
+    assert abs(cos.mean() - 2 / 3) < 0.03                             # cosine lobe: E[cos] = 2/3
+    # a point light ignores normal/side: same as the reference raygen
+    P = dict(pos=(1.0, 10.0, -2.0), rgb=(1, 1, 1), power=50.0)
+    o, d = oracle.emit_photon(P, 7)
+    assert np.array_equal(o, np.float32([1.0, 10.0, -2.0]))
+    st = np.array([oracle.lib.orc_lcg_init(7, 0)], np.uint32)
+    buf = (oracle.C.c_float * 3)()
+    s = oracle.C.c_uint32(int(st[0]))
+    oracle.lib.orc_random_point_in_unit_sphere(oracle.C.byref(s), buf)
+    assert np.array_equal(d, np.array(buf[:], np.float32))
