@@ -439,7 +439,7 @@ int pm_photon_map_destroy(pm_photon_map* m) {
 
 int pm_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int32_t k, float max_radius, int32_t* ids,
            float* d2, float* maxd2, void* stream) {
-  if (!m || nq < 0 || k < 1 || k > 128 || (nq > 0 && (!q || !ids)) || !(max_radius >= 0.f)) return PM_ERR_INVALID;
+  if (!m || nq < 0 || k < 1 || k > 256 || (nq > 0 && (!q || !ids)) || !(max_radius >= 0.f)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   PM_TRY_ST(launch_knn(m, q, nq, k, max_radius, ids, d2, maxd2, s));
   return map_err(hipStreamSynchronize(s));

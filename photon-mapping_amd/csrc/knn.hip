@@ -83,10 +83,12 @@ struct KnnCounters {
 //        bound ignores queued keys, i.e. it is never too tight: still exact.
 //  QL:   > 0 the same with a QL-deep per-lane LIFO queue in LDS (`lq`, this
 //        lane's column of a [QL][stride] array): deep batching without VGPRs.
+//  lo:   only keys > lo are candidates (multi-pass k > 128: pass p collects
+//        the 128 smallest keys above pass p-1's last; keys are unique).
 template <int K, bool POST, int QP, bool ST, int QL = 0>
 __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n, v3 q, float r2, bool valid,
                                          double (&list)[K], KnnCounters* kc = nullptr, double* lq = nullptr,
-                                         int lstride = 0) {
+                                         int lstride = 0, double lo = 0.0) {
   const double sentinel = key_make(r2, 0xFFFFFFFFu);
 #pragma unroll
   for (int j = 0; j < K; j++) list[j] = sentinel;
@@ -113,7 +115,7 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
         const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
         const float d2 = dx * dx + dy * dy + dz * dz;
         key = key_make(d2, (uint32_t)(w >> 2));
-        cand = d2 < r2 && key < list[K - 1];
+        cand = d2 < r2 && key < list[K - 1] && key > lo;
       }
       int next;
       if (prev == far_c) {
@@ -195,26 +197,30 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
   }
 }
 
+// pm_knn: K-wide list for k <= K; k > 128 runs 128-wide passes (j0 = output
+// offset of this pass, lo_in / lo_out = last key of the previous / this pass).
 template <int K, int QP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 64 ? 4 : 1))) void k_knn(const float4* nodes, int n, const pm_float3* q, int64_t nq, int k,
-                                             float r2, int32_t* ids, float* d2o, float* maxd2) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 64 ? 4 : 1))) void k_knn(
+    const float4* nodes, int n, const pm_float3* q, int64_t nq, int k, int j0, float r2, int32_t* ids, float* d2o,
+    float* maxd2, const double* lo_in, double* lo_out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < nq;
   double list[K];
   const pm_float3 p = valid ? q[i] : pm_float3{0.f, 0.f, 0.f};
-  knn_walk<K, true, QP, false>(nodes, n, mk(p), r2, valid, list);
+  const double lo = (valid && lo_in) ? lo_in[i] : 0.0;
+  knn_walk<K, true, QP, false>(nodes, n, mk(p), r2, valid, list, nullptr, nullptr, 0, lo);
   if (!valid) return;
-  double kth = list[0];
 #pragma unroll
   for (int j = 0; j < K; j++) {
-    if (j < k) {
+    const int jj = j0 + j;
+    if (jj < k) {
       const uint32_t id = key_id(list[j]);
-      ids[i * k + j] = id == 0xFFFFFFFFu ? -1 : (int32_t)id;
-      if (d2o) d2o[i * k + j] = key_d2(list[j]);
+      ids[i * k + jj] = id == 0xFFFFFFFFu ? -1 : (int32_t)id;
+      if (d2o) d2o[i * k + jj] = key_d2(list[j]);
     }
-    if (j == k - 1) kth = list[j];
+    if (jj == k - 1 && maxd2) maxd2[i] = key_d2(list[j]);
   }
-  if (maxd2) maxd2[i] = key_d2(kth);
+  if (lo_out) lo_out[i] = list[K - 1];
 }
 
 // Radiance estimate from a finished candidate list: gatherPhotons
@@ -328,10 +334,10 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
   const float r2 = radius * radius;
   const int n = (int)m->n;
   const int g = grid_for(nq, 256);
-#define PM_KNN_CASE(KK, QQ)                                                            \
-  if (k <= KK) {                                                                       \
-    k_knn<KK, QQ><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, r2, ids, d2, maxd2);      \
-    return hipGetLastError();                                                          \
+#define PM_KNN_CASE(KK, QQ)                                                                        \
+  if (k <= KK) {                                                                                   \
+    k_knn<KK, QQ><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, 0, r2, ids, d2, maxd2, nullptr, nullptr); \
+    return hipGetLastError();                                                                      \
   }
   PM_KNN_CASE(8, 0)
   PM_KNN_CASE(16, 0)
@@ -340,7 +346,15 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
   PM_KNN_CASE(64, 0)
   PM_KNN_CASE(128, 0)
 #undef PM_KNN_CASE
-  return hipErrorInvalidValue;
+  if (k > 256) return hipErrorInvalidValue;
+  // 128 < k <= 256: two exact 128-wide passes
+  DevBuf<double> lo(nq);
+  if (!lo.p) return hipErrorOutOfMemory;
+  k_knn<128, 0><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, 0, r2, ids, d2, maxd2, nullptr, lo.p);
+  PM_HIP_TRY(hipGetLastError());
+  k_knn<128, 0><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, 128, r2, ids, d2, maxd2, lo.p, nullptr);
+  PM_HIP_TRY(hipGetLastError());
+  return hipStreamSynchronize(s);   // lo is freed on return
 }
 
 hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,

@@ -255,6 +255,29 @@ def test_knn_and_gather_vs_oracle(cornell):
     assert np.array_equal(_bits(fg), _bits(fo))
 
 
+@pytest.mark.parametrize("k,radius", [(1, 100.0), (64, 100.0), (128, 100.0), (129, 100.0), (200, 100.0),
+                                      (256, 100.0), (200, 1.5)])
+def test_knn_k_range_vs_oracle(cornell, k, radius):
+    """pm_knn for every list width, incl. the two-pass path for 128 < k <= 256
+    (config 5 asks for k = 200) and a radius that leaves lists partly empty."""
+    import oracle
+    import pm_amd
+    meshes, lights = cornell
+    os_ = oracle.Scene(meshes)
+    g = oracle.trace(os_, lights, 10000, 10, False)
+    gm = pm_amd.PhotonMap(torch.from_numpy(g).cuda(), 1.0)
+    om = oracle.PhotonMap(g, 1.0)
+    rng = np.random.default_rng(k)
+    q = (g[rng.integers(0, len(g), 500), 0:3] + rng.normal(scale=0.5, size=(500, 3))).astype(np.float32)
+    ids, d2, md = pm_amd.knn(gm, torch.from_numpy(q).cuda(), k, radius)
+    oi, od, omd = om.knn(q, k, radius)
+    assert np.array_equal(ids.cpu().numpy(), oi)
+    assert np.array_equal(_bits(d2.cpu().numpy()), _bits(od))
+    assert np.array_equal(_bits(md.cpu().numpy()), _bits(omd))
+    if radius < 10:
+        assert (oi == -1).any()
+
+
 def test_photon_map_export(cornell):
     import oracle
     import pm_amd
