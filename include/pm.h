@@ -232,6 +232,22 @@ typedef struct {
 } pm_render_stats;
 int pm_render_stats_get(pm_render_stats* out);
 
+/* ---- photon viewer (photon-viewer/; debug splat) --------
+ * loadPhotons' projection (photon-viewer/src/hostCode.cu:53-75: glm lookAt x
+ * perspective(fovy, W/H, 0.1, 1000), z < 0 dropped, pixel = (int((x/w + 1)
+ * 0.5 W), H - int((y/w + 1) 0.5 H))) + photonViewerRayGen (photon-viewer/cuda/
+ * deviceCode.cu:10-38): a photon inside the frame whose visibility ray from
+ * look_from (tmin 0, tmax = |pos - eye| - 1e-4 in double) hits nothing paints
+ * make_rgba(color) over a 0xFF000000 frame. Several photons on one pixel: the
+ * highest index wins (the reference's order is a race). d_rgba is [H][W]. */
+typedef struct {
+  pm_float3 look_from, look_at, look_up;
+  float fovy;
+  int32_t width, height;
+} pm_viewer_params;
+int pm_photon_view(pm_scene* scene, const pm_photon* d_photons, int64_t n, const pm_viewer_params* params,
+                   uint32_t* d_rgba, void* stream);
+
 /* ---- host-side boundary I/O (no GPU needed) ------------------------------ */
 /* config.toml (configLoader.h:8-19; keys of photon-mapping/src/hostCode.cu:153-158
  * and ray-tracer/src/hostCode.cu:193-206). Strings are NUL-terminated. */

@@ -45,6 +45,11 @@ class Camera(C.Structure):
     _fields_ = [("pos", Float3), ("dir_00", Float3), ("dir_du", Float3), ("dir_dv", Float3)]
 
 
+class ViewerParams(C.Structure):
+    _fields_ = [("look_from", Float3), ("look_at", Float3), ("look_up", Float3), ("fovy", C.c_float),
+                ("width", C.c_int32), ("height", C.c_int32)]
+
+
 class TraceParams(C.Structure):
     _fields_ = [("casted_photons", C.c_int64), ("max_depth", C.c_int32), ("caustics_mode", C.c_int32),
                 ("shard_rank", C.c_int32), ("shard_count", C.c_int32)]
@@ -75,6 +80,8 @@ def _load():
         "orc_sinf": (C.c_float, [C.c_float]),
         "orc_cosf": (C.c_float, [C.c_float]),
         "orc_random_point_in_unit_sphere": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_float)]),
+        "orc_viewer_matrix": (None, [C.POINTER(ViewerParams), C.POINTER(C.c_float)]),
+        "orc_photon_view": (C.c_int, [_P, _P, C.c_int64, C.POINTER(ViewerParams), _P]),
         "orc_emit_photon": (None, [C.POINTER(Light), C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
         "orc_refract": (None, [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_float, C.POINTER(C.c_float)]),
         "orc_scene_create": (C.c_int, [C.POINTER(Mesh), C.c_int32, C.c_int32, C.POINTER(_P)]),
@@ -258,3 +265,21 @@ def render(scene: Scene, camera: Camera, w, h, spp, depth, sky, lights, gmap: Ph
     _chk(lib.orc_render(scene.h, C.byref(p), lights_array(lights), len(lights), gmap.h, cmap.h, lo, hi, nthreads,
                         rgba.ctypes.data, rgb.ctypes.data, C.byref(st)), "render")
     return rgba, rgb, st
+
+
+def viewer_params(look_from, look_at, look_up, fovy, w, h) -> ViewerParams:
+    return ViewerParams(_f3(look_from), _f3(look_at), _f3(look_up), float(fovy), int(w), int(h))
+
+
+def viewer_matrix(params: ViewerParams) -> np.ndarray:
+    """glm perspective * lookAt as the oracle builds it, column-major [4][4]."""
+    m = (C.c_float * 16)()
+    lib.orc_viewer_matrix(C.byref(params), m)
+    return np.array(m[:], np.float32).reshape(4, 4)
+
+
+def view_photons(scene: Scene, photons: np.ndarray, params: ViewerParams) -> np.ndarray:
+    ph = np.ascontiguousarray(photons, np.float32)
+    rgba = np.zeros((params.height, params.width), np.uint32)
+    _chk(lib.orc_photon_view(scene.h, ph.ctypes.data, len(ph), C.byref(params), rgba.ctypes.data), "photon_view")
+    return rgba

@@ -1106,3 +1106,70 @@ int orc_render(const orc_scene* s, const pm_render_params* p, const pm_light* li
   pthread_mutex_destroy(&C.mu);
   return PM_OK;
 }
+
+/* -------------------------------------------------------------------------- */
+/* Photon viewer (photon-viewer/src/hostCode.cu:53-75 projection with glm      */
+/* 0.9.9 lookAtRH / perspectiveRH_NO / mat4 products; photonViewerRayGen,     */
+/* photon-viewer/cuda/deviceCode.cu:10-38). Photons are painted in index order */
+/* so the highest index wins a shared pixel (the device's atomicMax rule).     */
+static float gdot(v3 a, v3 b) { const float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z; return tx + ty + tz; }
+static v3 gnorm(v3 v) { const float inv = 1.0f / sqrtf(gdot(v, v)); return V3(v.x * inv, v.y * inv, v.z * inv); }
+static v3 gcross(v3 x, v3 y) { return V3(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y); }
+
+void orc_viewer_matrix(const pm_viewer_params* P, float M[16]) {
+  const v3 eye = fromp(P->look_from), ctr = fromp(P->look_at), up = fromp(P->look_up);
+  const v3 f = gnorm(sub(ctr, eye));
+  const v3 s = gnorm(gcross(f, up));
+  const v3 u = gcross(s, f);
+  float V[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
+  V[0][0] = s.x; V[1][0] = s.y; V[2][0] = s.z;
+  V[0][1] = u.x; V[1][1] = u.y; V[2][1] = u.z;
+  V[0][2] = -f.x; V[1][2] = -f.y; V[2][2] = -f.z;
+  V[3][0] = -gdot(s, eye); V[3][1] = -gdot(u, eye); V[3][2] = gdot(f, eye);
+  const float aspect = (float)P->width / (float)P->height;
+  const float zn = 0.1f, zf = 1000.f;
+  const float th = tanf(P->fovy / 2.0f);
+  float Pm[4][4] = {{0}};
+  Pm[0][0] = 1.0f / (aspect * th);
+  Pm[1][1] = 1.0f / th;
+  Pm[2][2] = -(zf + zn) / (zf - zn);
+  Pm[2][3] = -1.0f;
+  Pm[3][2] = -(2.0f * zf * zn) / (zf - zn);
+  for (int i = 0; i < 4; i++)
+    for (int r = 0; r < 4; r++) {
+      float acc = Pm[0][r] * V[i][0];
+      acc = acc + Pm[1][r] * V[i][1];
+      acc = acc + Pm[2][r] * V[i][2];
+      acc = acc + Pm[3][r] * V[i][3];
+      M[4 * i + r] = acc;
+    }
+}
+
+int orc_photon_view(const orc_scene* s, const pm_photon* ph, int64_t n, const pm_viewer_params* P, uint32_t* rgba) {
+  if (!s || !P || P->width <= 0 || P->height <= 0 || !rgba) return PM_ERR_INVALID;
+  const int W = P->width, H = P->height;
+  for (int64_t i = 0; i < (int64_t)W * H; i++) rgba[i] = 0xFF000000u;
+  float M[16];
+  orc_viewer_matrix(P, M);
+  const v3 eye = fromp(P->look_from);
+  for (int64_t i = 0; i < n; i++) {
+    const pm_float3 p = ph[i].pos;
+    float c[4];
+    for (int r = 0; r < 4; r++) {
+      const float a0 = M[0 + r] * p.x + M[4 + r] * p.y;
+      const float a1 = M[8 + r] * p.z + M[12 + r];
+      c[r] = a0 + a1;
+    }
+    if (c[2] < 0.f) continue;
+    const float fx = (c[0] / c[3] + 1.f) * 0.5f * (float)W;
+    const float fy = (c[1] / c[3] + 1.f) * 0.5f * (float)H;
+    if (!(fx > -2147483648.f && fx < 2147483648.f) || !(fy > -2147483648.f && fy < 2147483648.f)) continue;
+    const int px = (int)fx, py = H - (int)fy;
+    if (px < 0 || px >= W || py < 0 || py >= H) continue;
+    const v3 d = V3(p.x - eye.x, p.y - eye.y, p.z - eye.z);
+    const float tmax = (float)(sqrt((double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z) - (double)1e-4f);
+    if (any_hit(s, eye, normalize(d), 0.0f, tmax)) continue;
+    rgba[px + (int64_t)W * py] = make_rgba(fromp(ph[i].color));
+  }
+  return PM_OK;
+}

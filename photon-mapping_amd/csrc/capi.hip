@@ -23,6 +23,8 @@ namespace pmd {
 
 hipError_t launch_query(pm_scene* sc, const pm_ray* rays, int64_t n, pm_hit* hits, int32_t* occ, bool any,
                         hipStream_t s);
+hipError_t photon_view(pm_scene* sc, const pm_photon* ph, int64_t n, const pm_viewer_params& P, uint32_t* rgba,
+                       hipStream_t s);
 hipError_t launch_trace_chunk(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl, int64_t g_lo,
                               int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt, hipStream_t s);
 hipError_t launch_compact(const pm_photon* slots, const uint32_t* cnt, const uint32_t* off, int64_t np,
@@ -498,6 +500,16 @@ int pm_render(pm_scene* sc, const pm_render_params* P, const pm_light* lights, i
   PM_TRY_ST(render_impl(sc, P, lights, nl, gmap, cmap, rgba, rgb, &stats, s));
   PM_TRY_ST(hipStreamSynchronize(s));
   g_render_stats = stats;
+  return check_overflow(sc, s);
+}
+
+int pm_photon_view(pm_scene* sc, const pm_photon* d_photons, int64_t n, const pm_viewer_params* P, uint32_t* d_rgba,
+                   void* stream) {
+  if (!sc || !P || n < 0 || (n > 0 && !d_photons) || n > INT32_MAX || P->width <= 0 || P->height <= 0 || !d_rgba)
+    return PM_ERR_INVALID;
+  if (int st = require_device()) return st;
+  hipStream_t s = (hipStream_t)stream;
+  PM_TRY_ST(photon_view(sc, d_photons, n, *P, d_rgba, s));
   return check_overflow(sc, s);
 }
 

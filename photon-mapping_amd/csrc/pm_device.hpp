@@ -385,6 +385,17 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
   return h;
 }
 
+// owl make_rgba: clamp(int(f * 256), 0, 255) per channel, alpha 0xff
+// (v_cvt_i32_f32 saturates; NaN -> 0).
+__device__ __forceinline__ uint32_t rgba_channel(float f) {
+  const float g = f * 256.f;
+  const int i = (g == g) ? (int)fminf(fmaxf(g, -2147483648.f), 2147483520.f) : 0;
+  return (uint32_t)min(255, max(0, i));
+}
+__device__ __forceinline__ uint32_t make_rgba(v3 c) {
+  return rgba_channel(c.x) | (rgba_channel(c.y) << 8) | (rgba_channel(c.z) << 16) | (0xFFu << 24);
+}
+
 // Photon emission. Point light: pointLightRayGen (photon-mapping/cuda/
 // deviceCode.cu:54-72), origin = light position, direction =
 // randomPointInUnitSphere. SQUARE_LIGHT (declared by the reference, world.h:

@@ -454,13 +454,7 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, const uint32_t* v
   const int y = A.H - py;
   if (y >= A.H) return;   // pixelID.y == 0 writes past the buffer in the reference: dropped
   const int64_t ofs = (int64_t)px + (int64_t)A.W * y;
-  // owl make_rgba: clamp(int(f*256), 0, 255), alpha 0xff (v_cvt_i32_f32 saturates, NaN -> 0)
-  auto q = [](float f) -> uint32_t {
-    const float g = f * 256.f;
-    int i = (g == g) ? (int)fminf(fmaxf(g, -2147483648.f), 2147483520.f) : 0;
-    return (uint32_t)min(255, max(0, i));
-  };
-  rgba[ofs] = q(fc.x) | (q(fc.y) << 8) | (q(fc.z) << 16) | (0xFFu << 24);
+  rgba[ofs] = make_rgba(fc);
   if (rgb) {
     rgb[3 * ofs] = fc.x;
     rgb[3 * ofs + 1] = fc.y;

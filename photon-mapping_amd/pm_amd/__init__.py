@@ -111,6 +111,11 @@ class RenderStats(C.Structure):
                 ("global_queries", C.c_int64), ("rays", C.c_int64)]
 
 
+class ViewerParams(C.Structure):  # pm_viewer_params (photon-viewer camera + fb_size)
+    _fields_ = [("look_from", Float3), ("look_at", Float3), ("look_up", Float3), ("fovy", C.c_float),
+                ("width", C.c_int32), ("height", C.c_int32)]
+
+
 class Config(C.Structure):
     _fields_ = [("look_from", Float3), ("look_at", Float3), ("look_up", Float3), ("fovy", C.c_float),
                 ("photons_file", C.c_char * 512), ("caustics_photons_file", C.c_char * 512),
@@ -156,6 +161,7 @@ _SIGNATURES = {
     "pm_camera_setup": (C.c_int, [Float3, Float3, Float3, C.c_float, C.c_int32, C.c_int32, C.POINTER(Camera)]),
     "pm_render": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Light), C.c_int32, _P, _P, _P, _P, _P]),
     "pm_render_stats_get": (C.c_int, [C.POINTER(RenderStats)]),
+    "pm_photon_view": (C.c_int, [_P, _P, C.c_int64, C.POINTER(ViewerParams), _P, _P]),
     "pm_config_load": (C.c_int, [C.c_char_p, C.POINTER(Config)]),
     "pm_config_key_name": (C.c_char_p, [C.c_int32]),
     "pm_scene_data_load": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
@@ -519,6 +525,18 @@ def render(scene: Scene, camera: Camera, width: int, height: int, spp: int, dept
     _check(_lib.pm_render(scene.handle, C.byref(p), la, len(lights), global_map.handle, caustic_map.handle,
                           _ptr(rgba), _ptr(rgb), _stream(stream)), "pm_render")
     return rgba, rgb
+
+
+def view_photons(scene: Scene, photons, look_from, look_at, look_up, fovy: float, width: int, height: int,
+                 stream=None):
+    """photonViewer run() (photon-viewer/src/hostCode.cu:109-154): splat a photon
+    array (N x 10 float32, device) onto a width x height RGBA8 image (int32 [H][W])."""
+    import torch
+    p = ViewerParams(_f3(look_from), _f3(look_at), _f3(look_up), float(fovy), int(width), int(height))
+    rgba = torch.empty((height, width), dtype=torch.int32, device="cuda")
+    _check(_lib.pm_photon_view(scene.handle, _ptr(photons), photons.shape[0], C.byref(p), _ptr(rgba),
+                               _stream(stream)), "pm_photon_view")
+    return rgba
 
 
 def render_stats() -> RenderStats:

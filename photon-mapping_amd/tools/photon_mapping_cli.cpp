@@ -7,6 +7,10 @@
 //   rayTracer       stage 2 (ray-tracer/src/hostCode.cu:180-245): read both
 //                   photon files, build the kd-trees, render, write
 //                   ray-tracer.output_filename (RGBA8 PNG, row H-y layout).
+//   photonViewer    photon-viewer/src/hostCode.cu:156-177: splat both photon
+//                   files onto photon-viewer.fb_size images (visibility rays),
+//                   written to photon-viewer.output_filename /
+//                   caustics_output_filename.
 //   photon-mapping  both stages in one process. The photon files are written
 //                   and read back, so the image equals the two-process
 //                   reference pipeline (the %.6f round trip quantises the
@@ -114,6 +118,23 @@ std::vector<pm_photon> read_photons(const char* path) {
   return v;
 }
 
+// photonViewer run() (photon-viewer/src/hostCode.cu:109-154) for one photon file
+int view_file(const pm_config& cfg, const Scene& sc, const char* photons_path, const char* out_path) {
+  const std::vector<pm_photon> ph = read_photons(photons_path);
+  const int W = cfg.viewer_fb_width, H = cfg.viewer_fb_height;
+  DevMem dp(sizeof(pm_photon) * (ph.size() ? ph.size() : 1)), fb(sizeof(uint32_t) * (size_t)W * (size_t)H);
+  check(pm_copy_to_device(dp.p, ph.data(), sizeof(pm_photon) * ph.size()), "photon upload");
+  pm_viewer_params vp{cfg.look_from, cfg.look_at, cfg.look_up, cfg.fovy, W, H};
+  check(pm_photon_view(sc.gpu, static_cast<pm_photon*>(dp.p), (int64_t)ph.size(), &vp, static_cast<uint32_t*>(fb.p),
+                       nullptr),
+        "photonViewerRayGen");
+  std::vector<uint32_t> h((size_t)W * (size_t)H);
+  check(pm_copy_to_host(h.data(), fb.p, sizeof(uint32_t) * h.size()), "framebuffer copy");
+  check(pm_write_png_rgba(out_path, h.data(), W, H), "stbi_write_png");
+  std::printf("Saved %s (%zu photons, %dx%d).\n", out_path, ph.size(), W, H);
+  return 0;
+}
+
 int stage_photons(const pm_config& cfg, const Scene& sc, std::vector<pm_photon>* g_out,
                   std::vector<pm_photon>* c_out) {
   std::vector<pm_photon> g = trace(sc, cfg, false);
@@ -187,8 +208,9 @@ bool require_keys(const pm_config& cfg, const std::vector<const char*>& keys) {
 
 void usage(const char* prog) {
   std::fprintf(stderr,
-               "usage: %s [--config PATH] [--stage photons|render|all] [--in-memory]\n"
-               "  photonMapping = --stage photons, rayTracer = --stage render, photon-mapping = --stage all\n",
+               "usage: %s [--config PATH] [--stage photons|render|all|view] [--in-memory]\n"
+               "  photonMapping = --stage photons, rayTracer = --stage render, photonViewer = --stage view,\n"
+               "  photon-mapping = --stage all\n",
                prog);
 }
 
@@ -198,7 +220,10 @@ int main(int argc, char** argv) {
   std::string name = argv[0];
   const size_t slash = name.find_last_of('/');
   if (slash != std::string::npos) name = name.substr(slash + 1);
-  std::string stage = name == "photonMapping" ? "photons" : (name == "rayTracer" ? "render" : "all");
+  std::string stage = name == "photonMapping" ? "photons"
+                      : name == "rayTracer"   ? "render"
+                      : name == "photonViewer" ? "view"
+                                               : "all";
   std::string config = "../config.toml";   // configLoader.h:6
   if (const char* e = std::getenv("PM_CONFIG")) config = e;
   bool in_memory = false;
@@ -215,7 +240,7 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
-  if (stage != "photons" && stage != "render" && stage != "all") {
+  if (stage != "photons" && stage != "render" && stage != "all" && stage != "view") {
     usage(argv[0]);
     return 2;
   }
@@ -230,7 +255,11 @@ int main(int argc, char** argv) {
   if (stage != "render")   // photon-mapping/src/hostCode.cu:153-158
     keys.insert(keys.end(), {"photon-mapper.casted_diffuse_photons", "photon-mapper.casted_caustics_photons",
                              "photon-mapper.max_depth"});
-  if (stage != "photons")  // ray-tracer/src/hostCode.cu:193-206
+  if (stage == "view")  // photon-viewer/src/hostCode.cu:114-120,160-164
+    keys = {"data.photons_file", "data.caustics_photons_file", "data.model_path", "camera.look_at",
+            "camera.look_from", "camera.look_up", "camera.fovy", "photon-viewer.output_filename",
+            "photon-viewer.caustics_output_filename", "photon-viewer.fb_size"};
+  else if (stage != "photons")  // ray-tracer/src/hostCode.cu:193-206
     keys.insert(keys.end(), {"camera.look_at", "camera.look_from", "camera.look_up", "camera.fovy",
                              "ray-tracer.sky_colour", "ray-tracer.output_filename", "ray-tracer.fb_size",
                              "ray-tracer.samples_per_pixel", "ray-tracer.depth"});
@@ -238,6 +267,10 @@ int main(int argc, char** argv) {
   Scene sc;
   load_scene(cfg, sc);
   if (stage == "photons") return stage_photons(cfg, sc, nullptr, nullptr);
+  if (stage == "view") {
+    view_file(cfg, sc, cfg.photons_file, cfg.viewer_output_filename);
+    return view_file(cfg, sc, cfg.caustics_photons_file, cfg.viewer_caustics_output_filename);
+  }
   std::vector<pm_photon> g, c;
   if (stage == "all") {
     stage_photons(cfg, sc, &g, &c);

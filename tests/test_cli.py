@@ -30,6 +30,11 @@ fb_size = [{w}, {h}]
 samples_per_pixel = 1
 depth = 30
 
+[photon-viewer]
+output_filename = "view.png"
+caustics_output_filename = "view_caustics.png"
+fb_size = [{w}, {h}]
+
 [photon-mapper]
 max_depth = 10
 casted_diffuse_photons = {casted}
@@ -49,7 +54,7 @@ def _run(name, cwd, *args):
 
 
 def test_cli_binaries_exist():
-    for name in ("photon-mapping", "photonMapping", "rayTracer"):
+    for name in ("photon-mapping", "photonMapping", "rayTracer", "photonViewer"):
         assert os.access(os.path.join(BIN, name), os.X_OK), name
 
 
@@ -106,6 +111,14 @@ def test_cli_two_stage_matches_oracle(tmp_path):
     # make_rgba quantises to 8 bits: the 1e-3 colour tolerance allows a 1-step difference
     assert np.abs(img.astype(int) - exp.astype(int)).max() <= 1
     assert np.mean(np.all(img == exp, axis=2)) >= 0.999
+
+    # photonViewer: both splats equal the oracle's
+    r4 = _run("photonViewer", run)
+    assert r4.returncode == 0, r4.stdout + r4.stderr
+    vp = oracle.viewer_params((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
+    for png, ph in (("view.png", gq), ("view_caustics.png", cq)):
+        got = np.array(Image.open(run / png)).reshape(H, W * 4).view(np.uint32).reshape(H, W)
+        assert np.array_equal(got, oracle.view_photons(os_, ph, vp)), png
 
     # the one-process binary reproduces the two-process result
     os.remove(run / "result.png")

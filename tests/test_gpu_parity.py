@@ -349,3 +349,19 @@ def test_render_empty_maps(cornell):
     cam = pm_amd.setup_camera((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, 32, 32)
     rgba, rgb = pm_amd.render(gs, cam, 32, 32, 1, 30, (1, 1, 1), lights, gmap, cmap)
     assert torch.isfinite(rgb).all()
+
+
+@pytest.mark.parametrize("caustics", [False, True])
+def test_photon_viewer_vs_oracle(cornell, caustics):
+    """photonViewer splat (pm_photon_view) equals the oracle image bit for bit."""
+    import oracle
+    import pm_amd
+    meshes, lights = cornell
+    os_ = oracle.Scene(meshes)
+    ph = oracle.trace(os_, lights, 20000, 10, caustics)
+    gs = pm_amd.Scene(meshes)
+    cam = ((80.0, 30.0, 0.0), (10.0, 20.0, 0.0), (0.0, 1.0, 0.0), 0.87)
+    img = pm_amd.view_photons(gs, torch.from_numpy(ph).cuda(), *cam, 160, 120).cpu().numpy().view(np.uint32)
+    ref = oracle.view_photons(os_, ph, oracle.viewer_params(*cam, 160, 120))
+    assert np.array_equal(img, ref)
+    assert (img != 0xFF000000).sum() > 50

@@ -312,3 +312,45 @@ def test_square_light_emission():
     s = oracle.C.c_uint32(int(st[0]))
     oracle.lib.orc_random_point_in_unit_sphere(oracle.C.byref(s), buf)
     assert np.array_equal(d, np.array(buf[:], np.float32))
+
+
+def test_viewer_projection():
+    """photonViewer projection (glm perspective x lookAt, hostCode.cu:53-75):
+    the oracle's float matrix agrees with a float64 evaluation of the glm
+    formulas; the look-at point lands on the centre pixel, a photon behind the
+    eye is dropped, an occluded one is not painted."""
+    import oracle
+    eye, ctr, up, fovy, W, H = (80.0, 30.0, 0.0), (10.0, 20.0, 0.0), (0.0, 1.0, 0.0), 0.87, 64, 48
+    P = oracle.viewer_params(eye, ctr, up, fovy, W, H)
+    M = oracle.viewer_matrix(P).astype(np.float64)          # column-major: M[col][row]
+    e, c, u = (np.array(v, np.float64) for v in (eye, ctr, up))
+    f = (c - e) / np.linalg.norm(c - e)
+    s = np.cross(f, u)
+    s /= np.linalg.norm(s)
+    uu = np.cross(s, f)
+    V = np.eye(4)
+    V[0, 0:3], V[1, 0:3], V[2, 0:3] = s, uu, -f            # rows of the view matrix
+    V[0:3, 3] = -s @ e, -uu @ e, f @ e
+    th = np.tan(fovy / 2)
+    Pm = np.zeros((4, 4))
+    Pm[0, 0], Pm[1, 1] = 1 / (W / H * th), 1 / th
+    Pm[2, 2], Pm[2, 3], Pm[3, 2] = -(1000.1) / (999.9), -2 * 1000 * 0.1 / 999.9, -1
+    ref = Pm @ V                                            # row-major
+    assert np.allclose(M.T, ref, rtol=1e-5, atol=1e-6)
+    empty = oracle.Scene([])
+    ph = np.zeros((3, 10), np.float32)
+    ph[0, 0:3] = ctr
+    ph[0, 7:10] = (1.0, 0.5, 0.25)
+    ph[1, 0:3] = (120.0, 30.0, 0.0)                         # behind the eye: clip z < 0
+    ph[1, 7:10] = 1.0
+    ph[2, 0:3] = (10.0, 60.0, 0.0)                          # outside the frame
+    img = oracle.view_photons(empty, ph, P)
+    painted = np.argwhere(img != 0xFF000000)
+    assert len(painted) == 1
+    y, x = painted[0]
+    assert abs(x - W / 2) <= 1 and abs(y - H / 2) <= 1
+    assert img[y, x] == (0xFF000000 | (64 << 16) | (128 << 8) | 255)
+    import pm_amd
+    wall = pm_amd.MeshData(np.float32([[40, -50, -50], [40, 50, -50], [40, 0, 50]]), np.int32([[0, 1, 2]]),
+                           np.float32([1, 1, 1, 1, 0, 0, 1]))
+    assert (oracle.view_photons(oracle.Scene([wall]), ph[:1], P) == 0xFF000000).all()
