@@ -285,6 +285,14 @@ int pm_photons_write_txt(const char* path, const pm_photon* h_photons, int64_t n
 int pm_photons_read_txt(const char* path, pm_photon** h_out, int64_t* n); /* free with pm_free */
 /* stbi_write_png(path, W, H, 4, rgba, W*4) (ray-tracer/src/hostCode.cu:240). */
 int pm_write_png_rgba(const char* path, const uint32_t* h_rgba, int32_t w, int32_t h);
+/* In-memory equivalent of write_txt -> read_txt on device photons: each of
+ * the 9 written floats becomes the float the %.6f text parses back to, power
+ * is zeroed (values with |x| >= 9e9 are outside the exact range). */
+int pm_photons_quantize(pm_photon* d_photons, int64_t n, void* stream);
+/* Binary photon file (faster than the text contract): "PMPHOTN1", int64 n,
+ * n x 40-B pm_photon records, little endian. */
+int pm_photons_write_bin(const char* path, const pm_photon* h_photons, int64_t n);
+int pm_photons_read_bin(const char* path, pm_photon** h_out, int64_t* n); /* free with pm_free */
 void pm_free(void* p);
 
 #ifdef __cplusplus

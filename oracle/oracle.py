@@ -80,6 +80,7 @@ def _load():
         "orc_sinf": (C.c_float, [C.c_float]),
         "orc_cosf": (C.c_float, [C.c_float]),
         "orc_random_point_in_unit_sphere": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_float)]),
+        "orc_quantize6": (None, [_P, _P, C.c_int64]),
         "orc_viewer_matrix": (None, [C.POINTER(ViewerParams), C.POINTER(C.c_float)]),
         "orc_photon_view": (C.c_int, [_P, _P, C.c_int64, C.POINTER(ViewerParams), _P]),
         "orc_emit_photon": (None, [C.POINTER(Light), C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
@@ -283,3 +284,10 @@ def view_photons(scene: Scene, photons: np.ndarray, params: ViewerParams) -> np.
     rgba = np.zeros((params.height, params.width), np.uint32)
     _chk(lib.orc_photon_view(scene.h, ph.ctypes.data, len(ph), C.byref(params), rgba.ctypes.data), "photon_view")
     return rgba
+
+
+def quantize6(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(x)
+    lib.orc_quantize6(x.ctypes.data, out.ctypes.data, x.size)
+    return out

@@ -1173,3 +1173,22 @@ int orc_photon_view(const orc_scene* s, const pm_photon* ph, int64_t n, const pm
   }
   return PM_OK;
 }
+
+/* %.6f text round trip without the text (see quantize6 in pm_device.hpp). */
+static float quantize6_pos(float a) {
+  const double m = rint((double)a * 1e6);
+  const double q = m / 1e6;
+  float f = (float)q;
+  const float fl = (double)f > q ? nextafterf(f, 0.0f) : f;
+  const float fh = nextafterf(fl, INFINITY);
+  const double mid = ((double)fl + (double)fh) * 0.5;
+  if (q == mid) {
+    const double r = fma(-q, 1e6, m);
+    if (r > 0) f = fh;
+    else if (r < 0) f = fl;
+  }
+  return f;
+}
+void orc_quantize6(const float* in, float* out, int64_t n) {
+  for (int64_t i = 0; i < n; i++) out[i] = signbit(in[i]) ? -quantize6_pos(-in[i]) : quantize6_pos(in[i]);
+}

@@ -76,6 +76,9 @@ int orc_render(const orc_scene* s, const pm_render_params* p, const pm_light* li
                int32_t row_lo, int32_t row_hi, int32_t nthreads,
                uint32_t* rgba, float* rgb, pm_render_stats* stats);
 
+/* The value each float takes after the %.6f text write + strtof read back. */
+void orc_quantize6(const float* in, float* out, int64_t n);
+
 /* Photon viewer splat (see pm_photon_view in include/pm.h). M is column-major. */
 void orc_viewer_matrix(const pm_viewer_params* params, float M[16]);
 int orc_photon_view(const orc_scene* s, const pm_photon* photons, int64_t n, const pm_viewer_params* params,

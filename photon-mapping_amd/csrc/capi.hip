@@ -23,6 +23,7 @@ namespace pmd {
 
 hipError_t launch_query(pm_scene* sc, const pm_ray* rays, int64_t n, pm_hit* hits, int32_t* occ, bool any,
                         hipStream_t s);
+hipError_t photons_quantize(pm_photon* ph, int64_t n, hipStream_t s);
 hipError_t photon_view(pm_scene* sc, const pm_photon* ph, int64_t n, const pm_viewer_params& P, uint32_t* rgba,
                        hipStream_t s);
 hipError_t launch_trace_chunk(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl, int64_t g_lo,
@@ -511,6 +512,12 @@ int pm_photon_view(pm_scene* sc, const pm_photon* d_photons, int64_t n, const pm
   hipStream_t s = (hipStream_t)stream;
   PM_TRY_ST(photon_view(sc, d_photons, n, *P, d_rgba, s));
   return check_overflow(sc, s);
+}
+
+int pm_photons_quantize(pm_photon* d, int64_t n, void* stream) {
+  if (n < 0 || (n > 0 && !d)) return PM_ERR_INVALID;
+  if (int st = require_device()) return st;
+  return map_err(photons_quantize(d, n, (hipStream_t)stream));
 }
 
 int pm_render_stats_get(pm_render_stats* o) {

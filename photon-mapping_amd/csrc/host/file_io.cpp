@@ -76,6 +76,42 @@ extern "C" int pm_photons_read_txt(const char* path, pm_photon** out, int64_t* n
   return PM_OK;
 }
 
+extern "C" int pm_photons_write_bin(const char* path, const pm_photon* ph, int64_t n) {
+  if (!path || (n > 0 && !ph) || n < 0) return PM_ERR_INVALID;
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return PM_ERR_IO;
+  const char magic[8] = {'P', 'M', 'P', 'H', 'O', 'T', 'N', '1'};
+  bool ok = std::fwrite(magic, 1, 8, f) == 8 && std::fwrite(&n, sizeof(n), 1, f) == 1 &&
+            (n == 0 || std::fwrite(ph, sizeof(pm_photon), (size_t)n, f) == (size_t)n);
+  ok = (std::fclose(f) == 0) && ok;
+  return ok ? PM_OK : PM_ERR_IO;
+}
+
+extern "C" int pm_photons_read_bin(const char* path, pm_photon** out, int64_t* n) {
+  if (!path || !out || !n) return PM_ERR_INVALID;
+  *out = nullptr;
+  *n = 0;
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return PM_ERR_IO;
+  char magic[8];
+  int64_t cnt = 0;
+  if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, "PMPHOTN1", 8) != 0 ||
+      std::fread(&cnt, sizeof(cnt), 1, f) != 1 || cnt < 0) {
+    std::fclose(f);
+    return PM_ERR_IO;
+  }
+  pm_photon* v = cnt ? (pm_photon*)std::malloc((size_t)cnt * sizeof(pm_photon)) : nullptr;
+  if (cnt && (!v || std::fread(v, sizeof(pm_photon), (size_t)cnt, f) != (size_t)cnt)) {
+    std::free(v);
+    std::fclose(f);
+    return PM_ERR_IO;
+  }
+  std::fclose(f);
+  *out = v;
+  *n = cnt;
+  return PM_OK;
+}
+
 namespace {
 void put32(std::vector<unsigned char>& o, uint32_t v) {
   o.push_back((unsigned char)(v >> 24));

@@ -385,6 +385,29 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
   return h;
 }
 
+// The %.6f text round trip of the two-process pipeline (writeAlivePhotons,
+// photon-mapping/src/hostCode.cu:31-49 -> readPhotonsFromFile, ray-tracer/src/
+// hostCode.cu:26-52) without the text: printf rounds the exact value to 6
+// decimals (ties to even) = rint(x * 1e6), exact in double (24 + 20 bits);
+// strtof returns the float nearest to m / 1e6: the double quotient rounded to
+// float, except when it sits exactly between two floats, where the sign of the
+// exact remainder fma(-q, 1e6, m) picks the side. Valid for |x| < 9e9.
+__host__ __device__ inline float quantize6_pos(float a) {
+  const double m = rint((double)a * 1e6);
+  const double q = m / 1e6;
+  float f = (float)q;
+  const float fl = (double)f > q ? nextafterf(f, 0.0f) : f;
+  const float fh = nextafterf(fl, INFINITY);
+  const double mid = ((double)fl + (double)fh) * 0.5;
+  if (q == mid) {
+    const double r = fma(-q, 1e6, m);
+    if (r > 0) f = fh;
+    else if (r < 0) f = fl;
+  }
+  return f;
+}
+__host__ __device__ inline float quantize6(float x) { return signbit(x) ? -quantize6_pos(-x) : quantize6_pos(x); }
+
 // owl make_rgba: clamp(int(f * 256), 0, 255) per channel, alpha 0xff
 // (v_cvt_i32_f32 saturates; NaN -> 0).
 __device__ __forceinline__ uint32_t rgba_channel(float f) {

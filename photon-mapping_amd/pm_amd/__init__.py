@@ -174,6 +174,9 @@ _SIGNATURES = {
     "pm_photons_write_txt": (C.c_int, [C.c_char_p, _P, C.c_int64]),
     "pm_photons_read_txt": (C.c_int, [C.c_char_p, C.POINTER(_P), C.POINTER(C.c_int64)]),
     "pm_write_png_rgba": (C.c_int, [C.c_char_p, _P, C.c_int32, C.c_int32]),
+    "pm_photons_quantize": (C.c_int, [_P, C.c_int64, _P]),
+    "pm_photons_write_bin": (C.c_int, [C.c_char_p, _P, C.c_int64]),
+    "pm_photons_read_bin": (C.c_int, [C.c_char_p, C.POINTER(_P), C.POINTER(C.c_int64)]),
     "pm_free": (None, [_P]),
 }
 
@@ -563,6 +566,30 @@ def read_photons_from_file(filename: str) -> np.ndarray:
     arr = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), (n.value * 10,)).reshape(-1, 10).copy()
     _lib.pm_free(p)
     return arr
+
+
+def quantize_photons(photons, stream=None):
+    """In place: the %.6f text round trip (write_alive_photons ->
+    read_photons_from_file) applied on the device."""
+    _check(_lib.pm_photons_quantize(_ptr(photons), photons.shape[0], _stream(stream)), "pm_photons_quantize")
+    return photons
+
+
+def write_photons_bin(photons: np.ndarray, filename: str):
+    ph = np.ascontiguousarray(photons, np.float32)
+    _check(_lib.pm_photons_write_bin(filename.encode(), ph.ctypes.data, len(ph)), "pm_photons_write_bin")
+
+
+def read_photons_bin(filename: str) -> np.ndarray:
+    h = _P()
+    n = C.c_int64()
+    _check(_lib.pm_photons_read_bin(filename.encode(), C.byref(h), C.byref(n)), "pm_photons_read_bin")
+    try:
+        if n.value == 0:
+            return np.zeros((0, 10), np.float32)
+        return np.ctypeslib.as_array(C.cast(h, C.POINTER(C.c_float)), (n.value * 10,)).reshape(-1, 10).copy()
+    finally:
+        _lib.pm_free(h)
 
 
 def write_png(filename: str, rgba: np.ndarray):

@@ -32,6 +32,9 @@ class FrameConfig:
     sky: tuple = (1.0, 1.0, 1.0)
     camera: dict = field(default_factory=lambda: dict(look_from=(80.0, 30.0, 0.0), look_at=(10.0, 20.0, 0.0),
                                                        look_up=(0.0, 1.0, 0.0), fovy=0.87))
+    # apply the %.6f photon-file round trip in memory (pm_photons_quantize), so
+    # the frame equals the reference's two-process pipeline
+    quantize: bool = False
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -80,6 +83,9 @@ class GpuBackend:
         self.phase["trace"] = self.phase.get("trace", 0.0) + pm.phase_us("trace") + pm.phase_us("compact")
         return t
 
+    def quantize(self, t):
+        return self.pm.quantize_photons(t)
+
     def maps(self, g, c):
         pm = self.pm
         gm = pm.PhotonMap(g, pm.PHOTON_POWER, c, pm.CAUSTICS_PHOTON_POWER)
@@ -111,6 +117,8 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
         if g.device.type == "cuda":
             torch.cuda.synchronize()
     backend.phase["exchange"] = (time.time() - te) * 1e6
+    if backend.cfg.quantize:
+        g, c = backend.quantize(g), backend.quantize(c)
     gm, cm = backend.maps(g, c)
     rgba = backend.render(gm, cm, rank, world, rgba)
     if world > 1:

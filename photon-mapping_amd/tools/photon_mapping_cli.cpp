@@ -12,9 +12,10 @@
 //                   written to photon-viewer.output_filename /
 //                   caustics_output_filename.
 //   photon-mapping  both stages in one process. The photon files are written
-//                   and read back, so the image equals the two-process
-//                   reference pipeline (the %.6f round trip quantises the
-//                   photons); --in-memory skips the round trip.
+//                   and their %.6f round trip is applied on the device
+//                   (pm_photons_quantize), so the image equals the two-process
+//                   reference pipeline; --in-memory renders the unquantised
+//                   photons.
 //
 // The config is ../config.toml relative to the working directory
 // (configLoader.h:6), overridable with --config PATH. All compute runs on the
@@ -147,12 +148,16 @@ int stage_photons(const pm_config& cfg, const Scene& sc, std::vector<pm_photon>*
 }
 
 int stage_render(const pm_config& cfg, const Scene& sc, const std::vector<pm_photon>& g,
-                 const std::vector<pm_photon>& c) {
+                 const std::vector<pm_photon>& c, bool quantize) {
   std::printf("Loaded %lld photons (non-caustic %lld, caustic %lld).\n", (long long)(g.size() + c.size()),
               (long long)g.size(), (long long)c.size());
   DevMem dg(sizeof(pm_photon) * (g.size() ? g.size() : 1)), dc(sizeof(pm_photon) * (c.size() ? c.size() : 1));
   check(pm_copy_to_device(dg.p, g.data(), sizeof(pm_photon) * g.size()), "photon upload");
   check(pm_copy_to_device(dc.p, c.data(), sizeof(pm_photon) * c.size()), "photon upload");
+  if (quantize) {   // the %.6f file round trip, applied on the device
+    check(pm_photons_quantize(static_cast<pm_photon*>(dg.p), (int64_t)g.size(), nullptr), "quantize");
+    check(pm_photons_quantize(static_cast<pm_photon*>(dc.p), (int64_t)c.size(), nullptr), "quantize");
+  }
   // loadPhotons (ray-tracer/src/hostCode.cu:54-99): global = diffuse (power 1)
   // ++ caustic (power 0.5); caustic map = caustic (power 0.5).
   pm_photon_map *gm = nullptr, *cm = nullptr;
@@ -273,14 +278,12 @@ int main(int argc, char** argv) {
   }
   std::vector<pm_photon> g, c;
   if (stage == "all") {
+    // the photon files are written as in the two-process pipeline; their %.6f
+    // round trip is applied in memory instead of re-parsing them
     stage_photons(cfg, sc, &g, &c);
-    if (!in_memory) {   // the two-process pipeline's %.6f round trip
-      g = read_photons(cfg.photons_file);
-      c = read_photons(cfg.caustics_photons_file);
-    }
-  } else {
-    g = read_photons(cfg.photons_file);
-    c = read_photons(cfg.caustics_photons_file);
+    return stage_render(cfg, sc, g, c, !in_memory);
   }
-  return stage_render(cfg, sc, g, c);
+  g = read_photons(cfg.photons_file);
+  c = read_photons(cfg.caustics_photons_file);
+  return stage_render(cfg, sc, g, c, false);
 }

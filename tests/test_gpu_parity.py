@@ -365,3 +365,21 @@ def test_photon_viewer_vs_oracle(cornell, caustics):
     ref = oracle.view_photons(os_, ph, oracle.viewer_params(*cam, 160, 120))
     assert np.array_equal(img, ref)
     assert (img != 0xFF000000).sum() > 50
+
+
+def test_quantize_matches_text_roundtrip(tmp_path):
+    """pm_photons_quantize (device) == write_alive_photons -> read_photons_from_file."""
+    import pm_amd
+    import test_host_io
+    v = test_host_io._quantize_corpus()
+    v = v[: len(v) // 9 * 9]
+    ph = np.zeros((len(v) // 9, 10), np.float32)
+    ph[:, 0:6] = v.reshape(-1, 9)[:, 0:6]
+    ph[:, 7:10] = v.reshape(-1, 9)[:, 6:9]
+    ph[:, 6] = np.float32(3.0)
+    p = str(tmp_path / "q.txt")
+    pm_amd.write_alive_photons(ph, p)
+    back = pm_amd.read_photons_from_file(p)
+    t = torch.from_numpy(ph.copy()).cuda()
+    pm_amd.quantize_photons(t)
+    assert np.array_equal(t.cpu().numpy().view(np.uint32), back.view(np.uint32))

@@ -200,3 +200,48 @@ def test_png_writer(tmp_path):
     im = np.array(Image.open(p))
     assert im.shape == (37, 53, 4)
     assert np.array_equal(im.reshape(37, 53 * 4).view(np.uint32).reshape(37, 53), rgba)
+
+
+def _quantize_corpus():
+    rng = np.random.default_rng(5)
+    v = np.concatenate([
+        rng.uniform(-50, 50, 200000), rng.normal(scale=1e-3, size=50000), rng.uniform(-1, 1, 50000),
+        rng.uniform(-2e4, 2e4, 50000),
+        # exact decimal ties at the 7th digit and their neighbours: k * 5e-7 in float
+        (np.arange(-20000, 20000) * 5e-7), np.float32(np.arange(1, 4000)) / np.float32(1024),
+        [0.0, -0.0, 1e-9, -1e-9, 5e-7, -5e-7, 1.5e-6, 0.0000015, 123456.789, -0.000000499, 9e8]]).astype(np.float32)
+    return v
+
+
+def test_quantize6_matches_text_roundtrip(tmp_path):
+    """orc_quantize6 (the algorithm of pm_photons_quantize) equals the %.6f
+    write + parse of writeAlivePhotons -> readPhotonsFromFile, sign of zero included."""
+    import oracle
+    import pm_amd
+    v = _quantize_corpus()
+    v = v[: len(v) // 9 * 9]
+    ph = np.zeros((len(v) // 9, 10), np.float32)
+    ph[:, 0:6] = v.reshape(-1, 9)[:, 0:6]
+    ph[:, 7:10] = v.reshape(-1, 9)[:, 6:9]
+    p = str(tmp_path / "q.txt")
+    pm_amd.write_alive_photons(ph, p)
+    back = pm_amd.read_photons_from_file(p)
+    q = oracle.quantize6(ph)
+    q[:, 6] = 0
+    assert np.array_equal(back.view(np.uint32), q.view(np.uint32))
+
+
+def test_binary_photon_file(tmp_path):
+    import pm_amd
+    rng = np.random.default_rng(6)
+    ph = rng.normal(size=(1001, 10)).astype(np.float32)
+    ph[:, 6] = rng.integers(0, 5, 1001).astype(np.int32).view(np.float32)
+    p = str(tmp_path / "p.bin")
+    pm_amd.write_photons_bin(ph, p)
+    assert os.path.getsize(p) == 16 + 1001 * 40
+    assert np.array_equal(pm_amd.read_photons_bin(p).view(np.uint32), ph.view(np.uint32))
+    pm_amd.write_photons_bin(ph[:0], p)
+    assert pm_amd.read_photons_bin(p).shape == (0, 10)
+    (tmp_path / "bad.bin").write_bytes(b"NOTPHOTN" + b"\0" * 8)
+    with pytest.raises(pm_amd.PMError):
+        pm_amd.read_photons_bin(str(tmp_path / "bad.bin"))
