@@ -232,6 +232,23 @@ typedef struct {
 } pm_render_stats;
 int pm_render_stats_get(pm_render_stats* out);
 
+/* pm_render in two halves, so that the map-independent half overlaps the
+ * photon trace and kd-tree build of the same frame (run it on another stream
+ * from another host thread). pm_render_begin traces the camera paths, the
+ * shadow and final-gather rays and the direct light, and sorts the gather
+ * queries; it reads only the scene. pm_render_finish runs the two gathers
+ * against the maps and resolves the pixels. begin + finish gives exactly
+ * pm_render's image. The job owns device memory until destroyed; finish may
+ * be called once. Overflow in either half is reported as PM_ERR_OVERFLOW. */
+typedef struct pm_render_job pm_render_job;
+int pm_render_begin(pm_scene* scene, const pm_render_params* params,
+                    const pm_light* lights, int32_t num_lights,
+                    pm_render_job** out, void* stream);
+int pm_render_finish(pm_render_job* job, const pm_photon_map* global_map,
+                     const pm_photon_map* caustic_map, uint32_t* d_rgba,
+                     float* d_rgb, void* stream);
+int pm_render_job_destroy(pm_render_job* job);
+
 /* ---- photon viewer (photon-viewer/; debug splat) --------
  * loadPhotons' projection (photon-viewer/src/hostCode.cu:53-75: glm lookAt x
  * perspective(fovy, W/H, 0.1, 1000), z < 0 dropped, pixel = (int((x/w + 1)

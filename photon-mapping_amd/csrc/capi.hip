@@ -38,9 +38,16 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
                       float* d2, float* maxd2, hipStream_t s);
 hipError_t launch_gather_api(const pm_photon_map* m, const pm_float3* pts, const float* brdf, int64_t nq,
                              pm_float3* out, hipStream_t s);
-hipError_t render_impl(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int nl,
-                       const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba, float* rgb,
-                       pm_render_stats* stats, hipStream_t s);
+hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int nl, pm_render_job* J,
+                        hipStream_t s);
+hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba,
+                         float* rgb, hipStream_t s);
+pm_render_job* render_job_new(pm_scene* sc);
+void render_job_delete(pm_render_job* J);
+const pm_render_stats& render_job_stats(const pm_render_job* J);
+pm_scene* render_job_scene(const pm_render_job* J);
+bool render_job_finished(const pm_render_job* J);
+void render_job_mark_finished(pm_render_job* J);
 
 namespace {
 std::mutex g_phase_mu;
@@ -257,6 +264,7 @@ int pm_scene_destroy(pm_scene* sc) {
 int pm_scene_intersect(pm_scene* sc, const pm_ray* rays, int64_t n, pm_hit* hits, void* stream) {
   if (!sc || n < 0 || (n > 0 && (!rays || !hits))) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
   PM_TRY_ST(launch_query(sc, rays, n, hits, nullptr, false, s));
   return check_overflow(sc, s);
 }
@@ -264,6 +272,7 @@ int pm_scene_intersect(pm_scene* sc, const pm_ray* rays, int64_t n, pm_hit* hits
 int pm_scene_occluded(pm_scene* sc, const pm_ray* rays, int64_t n, int32_t* occ, void* stream) {
   if (!sc || n < 0 || (n > 0 && (!rays || !occ))) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
   PM_TRY_ST(launch_query(sc, rays, n, nullptr, occ, true, s));
   return check_overflow(sc, s);
 }
@@ -319,6 +328,7 @@ int pm_trace_photons(pm_scene* sc, const pm_light* lights, int32_t nl, const pm_
   int st = shard_range(lights, nl, p, loff, lo, hi);
   if (st != PM_OK) return st;
   hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
   reset_phase(PH_TRACE);
   reset_phase(PH_COMPACT);
   const int maxd = p->max_depth;
@@ -381,6 +391,7 @@ int pm_kdtree_build(pm_kd_photon* d, int64_t n, pm_box* bounds, void* stream) {
   if (st != PM_OK) return st;
   if (n >= (1ll << 30)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
   reset_phase(PH_KDBUILD);
   PhaseTimer tm(PH_KDBUILD, s);
   return map_err(kd_build_records(d, n, bounds, s));
@@ -395,6 +406,7 @@ int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_phot
   const int64_t n = na + nb;
   if (n >= (1ll << 30)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
   pm_photon_map* m = new pm_photon_map;
   m->n = n;
   if (n > 0) {
@@ -431,6 +443,7 @@ int pm_photon_map_size(const pm_photon_map* m, int64_t* n) {
 int pm_photon_map_export(const pm_photon_map* m, pm_kd_photon* d_out, void* stream) {
   if (!m || (m->n > 0 && !d_out)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
   PM_TRY_ST(launch_map_export(m, d_out, s));
   return map_err(hipStreamSynchronize(s));
 }
@@ -444,6 +457,7 @@ int pm_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int32_t k, fl
            float* d2, float* maxd2, void* stream) {
   if (!m || nq < 0 || k < 1 || k > 256 || (nq > 0 && (!q || !ids)) || !(max_radius >= 0.f)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
   PM_TRY_ST(launch_knn(m, q, nq, k, max_radius, ids, d2, maxd2, s));
   return map_err(hipStreamSynchronize(s));
 }
@@ -452,6 +466,7 @@ int pm_gather(const pm_photon_map* m, const pm_float3* pts, const float* brdf, i
               void* stream) {
   if (!m || nq < 0 || (nq > 0 && (!pts || !brdf || !out))) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
   reset_phase(PH_GATHER);
   PhaseTimer tm(PH_GATHER, s);
   return map_err(launch_gather_api(m, pts, brdf, nq, out, s));
@@ -486,22 +501,66 @@ int pm_camera_setup(pm_float3 from, pm_float3 at, pm_float3 up, float fovy, int3
   return PM_OK;
 }
 
+static bool render_params_ok(const pm_scene* sc, const pm_render_params* P, const pm_light* lights, int32_t nl) {
+  return sc && P && nl >= 0 && (nl == 0 || lights) && P->width > 0 && P->height > 0 && P->samples_per_pixel > 0 &&
+         P->max_depth >= 0 && !(P->tile_count > 1 && (P->tile_rank < 0 || P->tile_rank >= P->tile_count));
+}
+
+int pm_render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int32_t nl, pm_render_job** out,
+                    void* stream) {
+  if (!out) return PM_ERR_INVALID;
+  *out = nullptr;
+  if (!render_params_ok(sc, P, lights, nl)) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  reset_phase(PH_PATHS);
+  pm_render_job* J = render_job_new(sc);
+  if (!J) return PM_ERR_OOM;
+  hipError_t e = render_begin(sc, P, lights, nl, J, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    render_job_delete(J);
+    return map_err(e);
+  }
+  const int st = check_overflow(sc, s);
+  if (st != PM_OK) {
+    render_job_delete(J);
+    return st;
+  }
+  *out = J;
+  return PM_OK;
+}
+
+int pm_render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba,
+                     float* rgb, void* stream) {
+  if (!J || !gmap || !cmap || !rgba || render_job_finished(J)) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  reset_phase(PH_GATHER); reset_phase(PH_RESOLVE); reset_phase(PH_GATHER_GLOBAL);
+  render_job_mark_finished(J);
+  PM_TRY_ST(render_finish(J, gmap, cmap, rgba, rgb, s));
+  PM_TRY_ST(hipStreamSynchronize(s));
+  {
+    std::lock_guard<std::mutex> lk(g_phase_mu);
+    g_render_stats = render_job_stats(J);
+  }
+  return check_overflow(render_job_scene(J), s);
+}
+
+int pm_render_job_destroy(pm_render_job* J) {
+  render_job_delete(J);
+  return PM_OK;
+}
+
 int pm_render(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int32_t nl,
               const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba, float* rgb, void* stream) {
-  if (!sc || !P || !gmap || !cmap || !rgba || nl < 0 || (nl > 0 && !lights) || P->width <= 0 || P->height <= 0 ||
-      P->samples_per_pixel <= 0 || P->max_depth < 0 || (P->tile_count > 1 && (P->tile_rank < 0 ||
-                                                                             P->tile_rank >= P->tile_count)))
-    return PM_ERR_INVALID;
-  hipStream_t s = (hipStream_t)stream;
-  reset_phase(PH_PATHS);
-  reset_phase(PH_GATHER);
-  reset_phase(PH_RESOLVE);
-  reset_phase(PH_GATHER_GLOBAL);
-  pm_render_stats stats{};
-  PM_TRY_ST(render_impl(sc, P, lights, nl, gmap, cmap, rgba, rgb, &stats, s));
-  PM_TRY_ST(hipStreamSynchronize(s));
-  g_render_stats = stats;
-  return check_overflow(sc, s);
+  if (!render_params_ok(sc, P, lights, nl) || !gmap || !cmap || !rgba) return PM_ERR_INVALID;
+  pm_render_job* J = nullptr;
+  int st = pm_render_begin(sc, P, lights, nl, &J, stream);
+  if (st != PM_OK) return st;
+  st = pm_render_finish(J, gmap, cmap, rgba, rgb, stream);
+  render_job_delete(J);
+  return st;
 }
 
 int pm_photon_view(pm_scene* sc, const pm_photon* d_photons, int64_t n, const pm_viewer_params* P, uint32_t* d_rgba,
@@ -510,6 +569,7 @@ int pm_photon_view(pm_scene* sc, const pm_photon* d_photons, int64_t n, const pm
     return PM_ERR_INVALID;
   if (int st = require_device()) return st;
   hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
   PM_TRY_ST(photon_view(sc, d_photons, n, *P, d_rgba, s));
   return check_overflow(sc, s);
 }
@@ -517,11 +577,13 @@ int pm_photon_view(pm_scene* sc, const pm_photon* d_photons, int64_t n, const pm
 int pm_photons_quantize(pm_photon* d, int64_t n, void* stream) {
   if (n < 0 || (n > 0 && !d)) return PM_ERR_INVALID;
   if (int st = require_device()) return st;
+  AllocStream alloc_scope((hipStream_t)stream);
   return map_err(photons_quantize(d, n, (hipStream_t)stream));
 }
 
 int pm_render_stats_get(pm_render_stats* o) {
   if (!o) return PM_ERR_INVALID;
+  std::lock_guard<std::mutex> lk(g_phase_mu);
   *o = g_render_stats;
   return PM_OK;
 }

@@ -8,10 +8,17 @@
 namespace pmd {
 
 // ------------------------------------------------------------ allocator
+// Free blocks are pooled per stream: a block returns to the pool of the stream
+// that is current (AllocStream) when it is freed, and is handed out again only
+// to work on that stream, so stream order makes reuse safe even when two host
+// threads drive two streams (pm_render_begin beside the photon trace). A block
+// that outlives an entry point is idle when freed (every entry point
+// synchronises its stream), so its pool does not matter.
 namespace {
 std::mutex g_mu;
-std::multimap<size_t, void*> g_free;           // size -> block
-std::unordered_map<void*, size_t> g_live;      // block -> size
+std::multimap<std::pair<hipStream_t, size_t>, void*> g_free;   // (stream, size) -> block
+std::unordered_map<void*, size_t> g_live;                      // block -> size
+thread_local hipStream_t t_stream = nullptr;
 size_t round_up(size_t b) {
   size_t r = 256;
   while (r < b) r <<= 1;
@@ -19,11 +26,14 @@ size_t round_up(size_t b) {
 }
 }  // namespace
 
+AllocStream::AllocStream(hipStream_t s) : prev(t_stream) { t_stream = s; }
+AllocStream::~AllocStream() { t_stream = prev; }
+
 void* dev_alloc(size_t bytes) {
   const size_t sz = round_up(bytes ? bytes : 1);
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto it = g_free.find(sz);
+    auto it = g_free.find({t_stream, sz});
     if (it != g_free.end()) {
       void* p = it->second;
       g_free.erase(it);
@@ -50,7 +60,7 @@ void dev_free(void* p) {
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_live.find(p);
   if (it == g_live.end()) return;
-  g_free.emplace(it->second, p);
+  g_free.emplace(std::make_pair(t_stream, it->second), p);
   g_live.erase(it);
 }
 

@@ -9,9 +9,18 @@
 
 namespace pmd {
 
-// Caching device allocator: freed blocks are kept and reused (stream-ordered
-// reuse on the library's single stream), so timed loops do not hipMalloc.
+// Caching device allocator: freed blocks are kept and reused in stream order
+// (per-stream pools, see prims.hip), so timed loops do not hipMalloc.
 void* dev_alloc(size_t bytes);
+// Sets the calling thread's current stream for dev_alloc / dev_free (RAII; one
+// per entry point).
+struct AllocStream {
+  hipStream_t prev;
+  explicit AllocStream(hipStream_t s);
+  ~AllocStream();
+  AllocStream(const AllocStream&) = delete;
+  AllocStream& operator=(const AllocStream&) = delete;
+};
 void dev_free(void* p);
 void dev_cache_trim();
 

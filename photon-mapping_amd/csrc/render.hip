@@ -22,6 +22,7 @@
 // diffuse rays' hit records are zero-initialised; a miss keeps the stale record.
 #include <algorithm>
 #include <cstring>
+#include <new>
 
 #include "pm_internal.hpp"
 
@@ -381,27 +382,40 @@ __global__ void k_unpermute_q(const float4* src, const uint32_t* perm, int64_t n
   dst[perm[i]] = src[i];
 }
 
-// Gather in Morton order of the query points (a pure permutation: results are
-// bitwise unchanged) so the lanes of a wave walk the same kd-tree nodes.
-static hipError_t sorted_gather(const pm_photon_map* m, const float4* dense, int64_t n, float4* res,
-                                const pm_box& bb, int tag, hipStream_t s) {
+// Gathers run in Morton order of the query points (a pure permutation:
+// results are bitwise unchanged) so the lanes of a wave walk the same kd-tree
+// nodes. The sort needs only the scene bounds, so it belongs to render_begin.
+struct SortedQueries {
+  DevBuf<uint32_t> keys, perm;
+  DevBuf<float4> qs, rs;
+  int64_t n = 0;
+};
+
+static hipError_t sort_queries(const float4* dense, int64_t n, const pm_box& bb, SortedQueries& Q, hipStream_t s) {
+  Q.n = n;
   if (n <= 0) return hipSuccess;
-  DevBuf<uint32_t> keys(n), perm(n);
-  DevBuf<float4> qs(n), rs(n);
-  if (!keys.p || !perm.p || !qs.p || !rs.p) return hipErrorOutOfMemory;
+  Q.keys.alloc(n);
+  Q.perm.alloc(n);
+  Q.qs.alloc(n);
+  Q.rs.alloc(n);
+  if (!Q.keys.p || !Q.perm.p || !Q.qs.p || !Q.rs.p) return hipErrorOutOfMemory;
   const float3 lo = make_float3(bb.lower.x, bb.lower.y, bb.lower.z);
   const float ex = bb.upper.x - bb.lower.x, ey = bb.upper.y - bb.lower.y, ez = bb.upper.z - bb.lower.z;
   const float3 inv = make_float3(ex > 0.f ? 1.0f / ex : 0.f, ey > 0.f ? 1.0f / ey : 0.f, ez > 0.f ? 1.0f / ez : 0.f);
-  k_query_morton<<<grid_for(n, 256), 256, 0, s>>>(dense, n, lo, inv, keys.p, perm.p);
+  k_query_morton<<<grid_for(n, 256), 256, 0, s>>>(dense, n, lo, inv, Q.keys.p, Q.perm.p);
   PM_HIP_TRY(hipGetLastError());
-  PM_HIP_TRY(radix_sort_pairs(keys.p, perm.p, n, 30, s));
-  k_permute_q<<<grid_for(n, 256), 256, 0, s>>>(dense, perm.p, n, qs.p);
-  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(radix_sort_pairs(Q.keys.p, Q.perm.p, n, 30, s));
+  k_permute_q<<<grid_for(n, 256), 256, 0, s>>>(dense, Q.perm.p, n, Q.qs.p);
+  return hipGetLastError();
+}
+
+static hipError_t gather_sorted(const pm_photon_map* m, SortedQueries& Q, float4* res, int tag, hipStream_t s) {
+  if (Q.n <= 0) return hipSuccess;
   {
     PhaseTimer tg(tag == 1 ? PH_GATHER_GLOBAL : PH_COUNT, s);
-    PM_HIP_TRY(launch_gather(m, qs.p, n, rs.p, s, tag));
+    PM_HIP_TRY(launch_gather(m, Q.qs.p, Q.n, Q.rs.p, s, tag));
   }
-  k_unpermute_q<<<grid_for(n, 256), 256, 0, s>>>(rs.p, perm.p, n, res);
+  k_unpermute_q<<<grid_for(Q.n, 256), 256, 0, s>>>(Q.rs.p, Q.perm.p, Q.n, res);
   return hipGetLastError();
 }
 
@@ -462,10 +476,43 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, const uint32_t* v
   }
 }
 
-hipError_t render_impl(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int nl,
-                       const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba, float* rgb,
-                       pm_render_stats* stats, hipStream_t s) {
-  RenderArgs A;
+}  // namespace pmd
+
+// Everything of a frame's render that does not depend on the photon maps:
+// camera paths, shadow / final-gather rays, direct light, compacted and
+// Morton-sorted gather queries. Held between pm_render_begin and
+// pm_render_finish so that it can overlap the photon trace and kd-tree build
+// (on another stream).
+struct pm_render_job {
+  pmd::RenderArgs A;
+  pmd::DevBuf<pmd::LightR> dl;
+  int64_t nthreads = 0, NV = 0, NG = 0, NS = 0;
+  pmd::DevBuf<uint32_t> cnt, voff, tot;
+  pmd::DevBuf<float4> vdirect, vatt, valb, cq, gq, galb, gdir, sray, sterm, cdense, gdense, cres, gres;
+  pmd::DevBuf<uint32_t> vflags, cvalid, gvalid, cidx, gidx, ctot, gtot, svis;
+  pmd::DevBuf<unsigned long long> rays;
+  pmd::SortedQueries cs, gs;
+  pm_render_stats stats{};
+  pm_scene* scene = nullptr;
+  bool finished = false;
+};
+
+namespace pmd {
+
+pm_render_job* render_job_new(pm_scene* sc) {
+  pm_render_job* J = new (std::nothrow) pm_render_job();
+  if (J) J->scene = sc;
+  return J;
+}
+void render_job_delete(pm_render_job* J) { delete J; }
+const pm_render_stats& render_job_stats(const pm_render_job* J) { return J->stats; }
+pm_scene* render_job_scene(const pm_render_job* J) { return J->scene; }
+bool render_job_finished(const pm_render_job* J) { return J->finished; }
+void render_job_mark_finished(pm_render_job* J) { J->finished = true; }
+
+hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int nl, pm_render_job* J,
+                        hipStream_t s) {
+  RenderArgs& A = J->A;
   A.W = P->width;
   A.H = P->height;
   A.spp = P->samples_per_pixel;
@@ -487,97 +534,125 @@ hipError_t render_impl(pm_scene* sc, const pm_render_params* P, const pm_light* 
     lh[i].pos = make_float4(lights[i].pos.x, lights[i].pos.y, lights[i].pos.z, (float)lights[i].power);
     lh[i].rgb = make_float4(lights[i].rgb.x, lights[i].rgb.y, lights[i].rgb.z, 0.f);
   }
-  DevBuf<LightR> dl(lh.size());
-  if (!dl.p) return hipErrorOutOfMemory;
-  PM_HIP_TRY(hipMemcpyAsync(dl.p, lh.data(), sizeof(LightR) * lh.size(), hipMemcpyHostToDevice, s));
-  A.lights = dl.p;
+  J->dl.alloc(lh.size());
+  if (!J->dl.p) return hipErrorOutOfMemory;
+  PM_HIP_TRY(hipMemcpyAsync(J->dl.p, lh.data(), sizeof(LightR) * lh.size(), hipMemcpyHostToDevice, s));
+  A.lights = J->dl.p;
   const int64_t nthreads = (int64_t)A.my_tiles * 256;
-  if (stats) std::memset(stats, 0, sizeof(*stats));
-  if (nthreads == 0) return hipSuccess;
+  J->nthreads = nthreads;
+  if (nthreads == 0) return hipStreamSynchronize(s);
   const DevScene S = sc->view();
-  DevBuf<uint32_t> cnt(nthreads), voff(nthreads), tot(1);
-  if (!cnt.p || !voff.p || !tot.p) return hipErrorOutOfMemory;
+  J->cnt.alloc(nthreads);
+  J->voff.alloc(nthreads);
+  J->tot.alloc(1);
+  if (!J->cnt.p || !J->voff.p || !J->tot.p) return hipErrorOutOfMemory;
   uint32_t V = 0;
   {
     PhaseTimer tm(PH_PATHS, s);
-    k_count_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, cnt.p, sc->overflow.p);
+    k_count_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, J->cnt.p, sc->overflow.p);
     PM_HIP_TRY(hipGetLastError());
-    PM_HIP_TRY(exclusive_scan_u32(cnt.p, voff.p, nthreads, tot.p, s));
-    PM_HIP_TRY(hipMemcpyAsync(&V, tot.p, 4, hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(exclusive_scan_u32(J->cnt.p, J->voff.p, nthreads, J->tot.p, s));
+    PM_HIP_TRY(hipMemcpyAsync(&V, J->tot.p, 4, hipMemcpyDeviceToHost, s));
     PM_HIP_TRY(hipStreamSynchronize(s));
   }
-  const int64_t NV = V, NG = (int64_t)V * kNumDiffuseSamples;
-  const int64_t NS = NV * nl;
-  DevBuf<float4> vdirect(NV), vatt(NV), valb(NV), cq(NV), gq(NG), galb(NG), gdir(NG), sray(NS), sterm(NS);
-  DevBuf<uint32_t> vflags(NV), cvalid(NV), gvalid(NG), cidx(NV), gidx(NG), ctot(1), gtot(1), svis(NS);
-  DevBuf<unsigned long long> rays(1);
-  if (NV > 0 && (!vdirect.p || !vatt.p || !valb.p || !cq.p || !gq.p || !galb.p || !vflags.p || !cvalid.p ||
-                 !gvalid.p || !cidx.p || !gidx.p || !gdir.p))
+  const int64_t NV = V, NG = (int64_t)V * kNumDiffuseSamples, NS = NV * nl;
+  J->NV = NV;
+  J->NG = NG;
+  J->NS = NS;
+  for (auto* b : {&J->vdirect, &J->vatt, &J->valb, &J->cq}) b->alloc(NV);
+  for (auto* b : {&J->gq, &J->galb, &J->gdir}) b->alloc(NG);
+  for (auto* b : {&J->vflags, &J->cvalid, &J->cidx}) b->alloc(NV);
+  for (auto* b : {&J->gvalid, &J->gidx}) b->alloc(NG);
+  J->sray.alloc(NS);
+  J->sterm.alloc(NS);
+  J->svis.alloc(NS);
+  J->ctot.alloc(1);
+  J->gtot.alloc(1);
+  J->rays.alloc(1);
+  if (NV > 0 && (!J->vdirect.p || !J->vatt.p || !J->valb.p || !J->cq.p || !J->gq.p || !J->galb.p ||
+                 !J->vflags.p || !J->cvalid.p || !J->gvalid.p || !J->cidx.p || !J->gidx.p || !J->gdir.p))
     return hipErrorOutOfMemory;
-  if (NS > 0 && (!sray.p || !sterm.p || !svis.p)) return hipErrorOutOfMemory;
-  PathOut O{vdirect.p, vatt.p, valb.p, vflags.p, cq.p, cvalid.p, gq.p, galb.p, gvalid.p,
-            gdir.p, sray.p, sterm.p, svis.p, rays.p};
+  if (NS > 0 && (!J->sray.p || !J->sterm.p || !J->svis.p)) return hipErrorOutOfMemory;
+  if (!J->ctot.p || !J->gtot.p || !J->rays.p) return hipErrorOutOfMemory;
+  PathOut O{J->vdirect.p, J->vatt.p, J->valb.p, J->vflags.p, J->cq.p,   J->cvalid.p, J->gq.p,
+            J->galb.p,    J->gvalid.p, J->gdir.p, J->sray.p,  J->sterm.p, J->svis.p,   J->rays.p};
   uint32_t NC = 0, NGv = 0;
   {
     PhaseTimer tm(PH_PATHS, s);
-    PM_HIP_TRY(hipMemsetAsync(rays.p, 0, 8, s));
-    k_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, voff.p, O, sc->overflow.p);
+    PM_HIP_TRY(hipMemsetAsync(J->rays.p, 0, 8, s));
+    k_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, J->voff.p, O, sc->overflow.p);
     PM_HIP_TRY(hipGetLastError());
     if (NG > 0) {
-      k_diffuse_rays<<<grid_for(NG, kRBlock), kRBlock, 0, s>>>(S, cq.p, gdir.p, NG, gvalid.p, gq.p, galb.p,
-                                                               sc->overflow.p);
+      k_diffuse_rays<<<grid_for(NG, kRBlock), kRBlock, 0, s>>>(S, J->cq.p, J->gdir.p, NG, J->gvalid.p, J->gq.p,
+                                                               J->galb.p, sc->overflow.p);
       PM_HIP_TRY(hipGetLastError());
     }
     if (NS > 0) {
-      k_shadow_rays<<<grid_for(NS, kRBlock), kRBlock, 0, s>>>(S, cq.p, sray.p, nl, NS, svis.p, sc->overflow.p);
+      k_shadow_rays<<<grid_for(NS, kRBlock), kRBlock, 0, s>>>(S, J->cq.p, J->sray.p, nl, NS, J->svis.p,
+                                                              sc->overflow.p);
       PM_HIP_TRY(hipGetLastError());
     }
     if (NV > 0) {
-      k_direct<<<grid_for(NV, 256), 256, 0, s>>>(A, NV, vflags.p, valb.p, sray.p, sterm.p, svis.p, vdirect.p);
+      k_direct<<<grid_for(NV, 256), 256, 0, s>>>(A, NV, J->vflags.p, J->valb.p, J->sray.p, J->sterm.p, J->svis.p,
+                                                 J->vdirect.p);
       PM_HIP_TRY(hipGetLastError());
     }
-    PM_HIP_TRY(exclusive_scan_u32(cvalid.p, cidx.p, NV, ctot.p, s));
-    PM_HIP_TRY(exclusive_scan_u32(gvalid.p, gidx.p, NG, gtot.p, s));
-    PM_HIP_TRY(hipMemcpyAsync(&NC, ctot.p, 4, hipMemcpyDeviceToHost, s));
-    PM_HIP_TRY(hipMemcpyAsync(&NGv, gtot.p, 4, hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(exclusive_scan_u32(J->cvalid.p, J->cidx.p, NV, J->ctot.p, s));
+    PM_HIP_TRY(exclusive_scan_u32(J->gvalid.p, J->gidx.p, NG, J->gtot.p, s));
+    PM_HIP_TRY(hipMemcpyAsync(&NC, J->ctot.p, 4, hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipMemcpyAsync(&NGv, J->gtot.p, 4, hipMemcpyDeviceToHost, s));
     PM_HIP_TRY(hipStreamSynchronize(s));
   }
-  DevBuf<float4> cdense(NC), gdense(NGv), cres(NC), gres(NGv);
-  if ((NC && (!cdense.p || !cres.p)) || (NGv && (!gdense.p || !gres.p))) return hipErrorOutOfMemory;
+  J->cdense.alloc(NC);
+  J->gdense.alloc(NGv);
+  J->cres.alloc(NC);
+  J->gres.alloc(NGv);
+  if ((NC && (!J->cdense.p || !J->cres.p)) || (NGv && (!J->gdense.p || !J->gres.p))) return hipErrorOutOfMemory;
   {
-    PhaseTimer tm(PH_GATHER, s);
+    PhaseTimer tm(PH_PATHS, s);
     if (NV) {
-      k_compact_q<<<grid_for(NV, 256), 256, 0, s>>>(cq.p, cvalid.p, cidx.p, NV, cdense.p);
+      k_compact_q<<<grid_for(NV, 256), 256, 0, s>>>(J->cq.p, J->cvalid.p, J->cidx.p, NV, J->cdense.p);
       PM_HIP_TRY(hipGetLastError());
-      k_compact_q<<<grid_for(NG, 256), 256, 0, s>>>(gq.p, gvalid.p, gidx.p, NG, gdense.p);
+      k_compact_q<<<grid_for(NG, 256), 256, 0, s>>>(J->gq.p, J->gvalid.p, J->gidx.p, NG, J->gdense.p);
       PM_HIP_TRY(hipGetLastError());
     }
-    PM_HIP_TRY(sorted_gather(cmap, cdense.p, NC, cres.p, sc->bounds, 0, s));
-    PM_HIP_TRY(sorted_gather(gmap, gdense.p, NGv, gres.p, sc->bounds, 1, s));
-  }
-  {
-    PhaseTimer tm(PH_RESOLVE, s);
-    k_resolve<<<grid_for(nthreads, 256), 256, 0, s>>>(A, voff.p, cnt.p, O, cidx.p, cres.p, gidx.p, gres.p, rgba,
-                                                      rgb);
-    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(sort_queries(J->cdense.p, NC, sc->bounds, J->cs, s));
+    PM_HIP_TRY(sort_queries(J->gdense.p, NGv, sc->bounds, J->gs, s));
   }
   unsigned long long nr = 0;
-  PM_HIP_TRY(hipMemcpyAsync(&nr, rays.p, 8, hipMemcpyDeviceToHost, s));
+  PM_HIP_TRY(hipMemcpyAsync(&nr, J->rays.p, 8, hipMemcpyDeviceToHost, s));
   PM_HIP_TRY(hipStreamSynchronize(s));
-  if (stats) {
-    int64_t px = 0;
-    for (int64_t t = 0; t < A.my_tiles; t++) {
-      const int64_t tile = A.tile_rank + t * A.tile_count;
-      const int ty = (int)(tile / A.tiles_x), tx = (int)(tile % A.tiles_x);
-      px += (int64_t)std::min(16, A.W - tx * 16) * std::min(16, A.H - ty * 16);
-    }
-    stats->pixels = px;
-    stats->path_vertices = NV;
-    stats->caustic_queries = NC;
-    stats->global_queries = NGv;
-    stats->rays = (int64_t)nr;
+  int64_t px = 0;
+  for (int64_t t = 0; t < A.my_tiles; t++) {
+    const int64_t tile = A.tile_rank + t * A.tile_count;
+    const int ty = (int)(tile / A.tiles_x), tx = (int)(tile % A.tiles_x);
+    px += (int64_t)std::min(16, A.W - tx * 16) * std::min(16, A.H - ty * 16);
   }
+  J->stats.pixels = px;
+  J->stats.path_vertices = NV;
+  J->stats.caustic_queries = NC;
+  J->stats.global_queries = NGv;
+  J->stats.rays = (int64_t)nr;
   return hipSuccess;
+}
+
+hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba,
+                         float* rgb, hipStream_t s) {
+  if (J->nthreads == 0) return hipSuccess;
+  {
+    PhaseTimer tm(PH_GATHER, s);
+    PM_HIP_TRY(gather_sorted(cmap, J->cs, J->cres.p, 0, s));
+    PM_HIP_TRY(gather_sorted(gmap, J->gs, J->gres.p, 1, s));
+  }
+  PathOut O{J->vdirect.p, J->vatt.p, J->valb.p, J->vflags.p, J->cq.p,   J->cvalid.p, J->gq.p,
+            J->galb.p,    J->gvalid.p, J->gdir.p, J->sray.p,  J->sterm.p, J->svis.p,   J->rays.p};
+  {
+    PhaseTimer tm(PH_RESOLVE, s);
+    k_resolve<<<grid_for(J->nthreads, 256), 256, 0, s>>>(J->A, J->voff.p, J->cnt.p, O, J->cidx.p, J->cres.p,
+                                                         J->gidx.p, J->gres.p, rgba, rgb);
+    PM_HIP_TRY(hipGetLastError());
+  }
+  return hipStreamSynchronize(s);
 }
 
 }  // namespace pmd

@@ -161,6 +161,9 @@ _SIGNATURES = {
     "pm_camera_setup": (C.c_int, [Float3, Float3, Float3, C.c_float, C.c_int32, C.c_int32, C.POINTER(Camera)]),
     "pm_render": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Light), C.c_int32, _P, _P, _P, _P, _P]),
     "pm_render_stats_get": (C.c_int, [C.POINTER(RenderStats)]),
+    "pm_render_begin": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Light), C.c_int32, C.POINTER(_P), _P]),
+    "pm_render_finish": (C.c_int, [_P, _P, _P, _P, _P, _P]),
+    "pm_render_job_destroy": (C.c_int, [_P]),
     "pm_photon_view": (C.c_int, [_P, _P, C.c_int64, C.POINTER(ViewerParams), _P, _P]),
     "pm_config_load": (C.c_int, [C.c_char_p, C.POINTER(Config)]),
     "pm_config_key_name": (C.c_char_p, [C.c_int32]),
@@ -528,6 +531,48 @@ def render(scene: Scene, camera: Camera, width: int, height: int, spp: int, dept
     _check(_lib.pm_render(scene.handle, C.byref(p), la, len(lights), global_map.handle, caustic_map.handle,
                           _ptr(rgba), _ptr(rgb), _stream(stream)), "pm_render")
     return rgba, rgb
+
+
+class RenderJob:
+    """pm_render_begin's map-independent half of a render (camera paths, shadow
+    and final-gather rays, direct light, sorted gather queries). It reads only
+    the scene, so it may run on another stream and host thread (ctypes releases
+    the GIL) while the photons are traced and the kd-trees built; finish() runs
+    the gathers and resolve. begin + finish == render()."""
+
+    def __init__(self, scene: Scene, camera: Camera, width: int, height: int, spp: int, depth: int, sky, lights,
+                 tile_rank: int = 0, tile_count: int = 1, stream=None):
+        self.width, self.height = int(width), int(height)
+        self._scene = scene   # keeps the scene alive while the job refers to it
+        p = RenderParams(self.width, self.height, int(spp), int(depth), camera, _f3(sky), int(tile_rank),
+                         int(tile_count))
+        la = lights_array(lights)
+        h = _P()
+        _check(_lib.pm_render_begin(scene.handle, C.byref(p), la, len(lights), C.byref(h), _stream(stream)),
+               "pm_render_begin")
+        self._h = h.value
+
+    def finish(self, global_map: PhotonMap, caustic_map: PhotonMap, want_rgb: bool = True, rgba=None, stream=None):
+        import torch
+        if rgba is None:
+            rgba = torch.zeros((self.height, self.width), dtype=torch.int32, device="cuda")
+        rgb = torch.zeros((self.height, self.width, 3), dtype=torch.float32, device="cuda") if want_rgb else None
+        _check(_lib.pm_render_finish(self._h, global_map.handle, caustic_map.handle, _ptr(rgba), _ptr(rgb),
+                                     _stream(stream)), "pm_render_finish")
+        return rgba, rgb
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.pm_render_job_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def render_begin(scene: Scene, camera: Camera, width: int, height: int, spp: int, depth: int, sky, lights,
+                 tile_rank: int = 0, tile_count: int = 1, stream=None) -> RenderJob:
+    return RenderJob(scene, camera, width, height, spp, depth, sky, lights, tile_rank, tile_count, stream)
 
 
 def view_photons(scene: Scene, photons, look_from, look_at, look_up, fovy: float, width: int, height: int,

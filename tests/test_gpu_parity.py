@@ -383,3 +383,51 @@ def test_quantize_matches_text_roundtrip(tmp_path):
     t = torch.from_numpy(ph.copy()).cuda()
     pm_amd.quantize_photons(t)
     assert np.array_equal(t.cpu().numpy().view(np.uint32), back.view(np.uint32))
+
+
+def test_render_begin_finish_equals_render(cornell):
+    """pm_render_begin + pm_render_finish (on a different stream) give exactly
+    pm_render's image and stats; a job finishes once."""
+    import pm_amd
+    meshes, lights = cornell
+    gs = pm_amd.Scene(meshes)
+    gph = pm_amd.run_point_light_ray_gen(gs, lights, 20000, 10, False)
+    cph = pm_amd.run_caustics(gs, lights, 20000, 10)
+    gmap, cmap = pm_amd.load_photons(gph, cph)
+    W, H = 56, 40
+    cam = pm_amd.setup_camera((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
+    rgba, rgb = pm_amd.render(gs, cam, W, H, 2, 30, (1, 1, 1), lights, gmap, cmap)
+    st = pm_amd.render_stats()
+    side = torch.cuda.Stream()
+    job = pm_amd.render_begin(gs, cam, W, H, 2, 30, (1, 1, 1), lights, stream=side.cuda_stream)
+    rgba2, rgb2 = job.finish(gmap, cmap)
+    st2 = pm_amd.render_stats()
+    assert torch.equal(rgba, rgba2)
+    assert np.array_equal(_bits(rgb.cpu().numpy()), _bits(rgb2.cpu().numpy()))
+    assert bytes(st) == bytes(st2)
+    with pytest.raises(pm_amd.PMError):
+        job.finish(gmap, cmap)
+    job.close()
+
+
+def test_frame_overlap_matches_serial(cornell):
+    """The frame driver with pm_render_begin on a worker thread + side stream
+    (overlapping trace and kd build) renders the serial frame bit for bit,
+    frame after frame (the per-stream allocator pools keep reuse safe)."""
+    import pm_amd
+    from pm_amd import dist as pmdist
+    meshes, lights = cornell
+    gs = pm_amd.Scene(meshes)
+    imgs = {}
+    for overlap in (False, True):
+        cfg = pmdist.FrameConfig(casted=40000, caustic=20000, width=64, height=48, overlap_render=overlap,
+                                 overlap_at="build")
+        be = pmdist.GpuBackend(gs, lights, cfg, 0, 1)
+        rgba = torch.zeros((cfg.height, cfg.width), dtype=torch.int32, device="cuda")
+        for it in range(3):
+            rgba.zero_()
+            out, info = pmdist.frame(be, 0, 1, None, rgba)
+            torch.cuda.synchronize()
+            imgs.setdefault(overlap, []).append(out.cpu().clone())
+    for a in imgs[False] + imgs[True]:
+        assert torch.equal(a, imgs[False][0])
