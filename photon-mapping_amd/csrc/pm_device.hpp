@@ -277,7 +277,13 @@ constexpr int kStackDepth = PM_STACK_DEPTH;
 #define PM_PATHS_WAVES 0   // fused render kernel: 5 helped (45.5 -> 42.7 ms); after the ray split the default is as good
 #endif
 #define PM_WAVES_ATTR(w) __attribute__((amdgpu_waves_per_eu((w) > 0 ? (w) : 1, (w) > 0 ? (w) : 10)))
+// PM_NO_SPILL: LDS stack only (no private scratch in any traversal kernel);
+// rays deeper than kStackDepth report PM_ERR_OVERFLOW. A/B and diagnostics.
+#ifdef PM_NO_SPILL
+constexpr int kSpillDepth = 0;
+#else
 constexpr int kSpillDepth = 64 - PM_STACK_DEPTH > 0 ? 64 - PM_STACK_DEPTH : 1;
+#endif
 constexpr int32_t kBvhEmpty = INT32_MIN;
 
 struct HitInfo {
@@ -325,7 +331,7 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
                                             int stride, int* overflow) {
   HitInfo h{tmax, -1, -1};
   if (S.ntri <= 0) return h;
-  int spill[kSpillDepth];
+  int spill[kSpillDepth > 0 ? kSpillDepth : 1];
   int sp = 0;
   int node = 0;
   for (;;) {
@@ -364,7 +370,7 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
         if (cnt > 3) stack[(sp++) * stride] = c3;
         if (cnt > 2) stack[(sp++) * stride] = c2;
         if (cnt > 1) stack[(sp++) * stride] = c1;
-      } else {
+      } else if (kSpillDepth > 0) {
 #pragma unroll
         for (int k = 0; k < 3; k++) {
           const int c = k == 0 ? c3 : (k == 1 ? c2 : c1);
@@ -380,7 +386,7 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
     }
     if (sp == 0) break;
     sp--;
-    node = sp < kStackDepth ? stack[sp * stride] : spill[sp - kStackDepth];
+    node = (kSpillDepth == 0 || sp < kStackDepth) ? stack[sp * stride] : spill[sp - kStackDepth];
   }
   return h;
 }

@@ -8,9 +8,7 @@ over RCCL ("nccl" backend) on MI355X, gloo on CPU for tests.
                 buffers); rank-order concatenation reproduces the 1-GPU array.
   3. build      every rank builds the same kd-trees (replicated; cheaper than a
                 second exchange).
-  4. render     16x16 image tiles dealt round robin (tile % G == r). The
-                map-independent half (pm_render_begin) runs on a side stream
-                from a worker thread, overlapping steps 1-3.
+  4. render     16x16 image tiles dealt round robin (tile % G == r).
   5. assemble   tiles are disjoint, so an integer SUM-reduce to rank 0 merges
                 the RGBA8 image exactly.
 The compute backend is pluggable: `GpuBackend` (libpm_hip.so) in production;
@@ -18,7 +16,6 @@ tests plug the CPU oracle in to check the orchestration with gloo.
 """
 from __future__ import annotations
 
-import os
 import time
 from dataclasses import dataclass, field
 
@@ -38,10 +35,6 @@ class FrameConfig:
     # apply the %.6f photon-file round trip in memory (pm_photons_quantize), so
     # the frame equals the reference's two-process pipeline
     quantize: bool = False
-    # run pm_render_begin (camera paths, rays, direct light: map-independent)
-    # on a second stream and host thread, beside the photon trace + kd build
-    overlap_render: bool = False   # see DESIGN §6: on only once proven safe
-    overlap_at: str = "build"
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -101,49 +94,6 @@ class GpuBackend:
         self.phase["kdbuild"] = kd + pm.phase_us("kdbuild")
         return gm, cm
 
-    def start_render(self, tile_rank: int, tile_count: int):
-        """pm_render_begin on a side stream from a worker thread (ctypes drops the
-        GIL, so the main thread keeps launching the trace and kd build)."""
-        import threading
-        import torch
-        pm, c = self.pm, self.cfg
-        dev = torch.cuda.current_device()
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=dev)
-        box = {}
-        # PM_OVERLAP_STREAM=null: worker thread on the null stream (host overlap only; A/B)
-        side_handle = 0 if os.environ.get("PM_OVERLAP_STREAM") == "null" else self._side.cuda_stream
-
-        def work():
-            try:
-                torch.cuda.set_device(dev)   # the current device is per host thread
-                box["job"] = pm.render_begin(self.scene, self.cam, c.width, c.height, c.spp, c.depth, c.sky,
-                                             self.lights, tile_rank=tile_rank, tile_count=tile_count,
-                                             stream=side_handle)
-                box["paths"] = pm.phase_us("paths")
-            except BaseException as e:   # re-raised on the main thread in finish_render
-                box["err"] = e
-
-        th = threading.Thread(target=work, name="pm-render-begin", daemon=True)
-        th.start()
-        return th, box
-
-    def finish_render(self, pending, gm, cm, rgba):
-        th, box = pending
-        th.join()
-        if "err" in box:
-            raise box["err"]
-        job = box["job"]
-        try:
-            job.finish(gm, cm, want_rgb=False, rgba=rgba)
-        finally:
-            job.close()
-        pm = self.pm
-        self.phase["paths"] = box["paths"]
-        for k in ("gather", "gather_global", "resolve"):
-            self.phase[k] = pm.phase_us(k)
-        return rgba
-
     def render(self, gm, cm, tile_rank: int, tile_count: int, rgba):
         pm = self.pm
         c = self.cfg
@@ -158,16 +108,6 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     """One frame through `backend`; returns (rgba on rank 0 (merged), info)."""
     import torch
     backend.phase = {}
-    pending = None
-    overlap = getattr(backend.cfg, "overlap_render", False)
-    if os.environ.get("PM_OVERLAP") is not None:
-        overlap = os.environ["PM_OVERLAP"] != "0"
-    # where the map-independent render half starts: "trace" (beside trace + kd
-    # build) or "build" (beside the kd build only, whose kernels use no scratch)
-    overlap_at = os.environ.get("PM_OVERLAP_AT", getattr(backend.cfg, "overlap_at", "build"))
-    overlap = overlap and hasattr(backend, "start_render")
-    if overlap and overlap_at == "trace":
-        pending = backend.start_render(rank, world)
     g = backend.trace(False, rank, world)
     c = backend.trace(True, rank, world)
     te = time.time()
@@ -179,13 +119,8 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     backend.phase["exchange"] = (time.time() - te) * 1e6
     if backend.cfg.quantize:
         g, c = backend.quantize(g), backend.quantize(c)
-    if overlap and pending is None:
-        pending = backend.start_render(rank, world)
     gm, cm = backend.maps(g, c)
-    if pending is not None:
-        rgba = backend.finish_render(pending, gm, cm, rgba)
-    else:
-        rgba = backend.render(gm, cm, rank, world, rgba)
+    rgba = backend.render(gm, cm, rank, world, rgba)
     if world > 1:
         dist.reduce(rgba, dst=0, op=dist.ReduceOp.SUM)
     info = {"n_global": int(gm.n), "n_caustic": int(cm.n), "n_global_rows": int(g.shape[0]),

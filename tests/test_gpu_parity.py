@@ -410,24 +410,25 @@ def test_render_begin_finish_equals_render(cornell):
     job.close()
 
 
-def test_frame_overlap_matches_serial(cornell):
-    """The frame driver with pm_render_begin on a worker thread + side stream
-    (overlapping trace and kd build) renders the serial frame bit for bit,
-    frame after frame (the per-stream allocator pools keep reuse safe)."""
+def test_frame_driver_matches_direct_pipeline(cornell):
+    """dist.frame over GpuBackend (world 1) renders exactly the image of the
+    direct pm_amd calls (trace -> maps -> render), frame after frame."""
     import pm_amd
     from pm_amd import dist as pmdist
     meshes, lights = cornell
     gs = pm_amd.Scene(meshes)
-    imgs = {}
-    for overlap in (False, True):
-        cfg = pmdist.FrameConfig(casted=40000, caustic=20000, width=64, height=48, overlap_render=overlap,
-                                 overlap_at="build")
-        be = pmdist.GpuBackend(gs, lights, cfg, 0, 1)
-        rgba = torch.zeros((cfg.height, cfg.width), dtype=torch.int32, device="cuda")
-        for it in range(3):
-            rgba.zero_()
-            out, info = pmdist.frame(be, 0, 1, None, rgba)
-            torch.cuda.synchronize()
-            imgs.setdefault(overlap, []).append(out.cpu().clone())
-    for a in imgs[False] + imgs[True]:
-        assert torch.equal(a, imgs[False][0])
+    cfg = pmdist.FrameConfig(casted=40000, caustic=20000, width=64, height=48)
+    g = pm_amd.run_point_light_ray_gen(gs, lights, cfg.casted, cfg.max_depth, False)
+    c = pm_amd.run_point_light_ray_gen(gs, lights, cfg.caustic, cfg.max_depth, True)
+    gmap, cmap = pm_amd.load_photons(g, c)
+    cam = pm_amd.setup_camera(cfg.camera["look_from"], cfg.camera["look_at"], cfg.camera["look_up"],
+                              cfg.camera["fovy"], cfg.width, cfg.height)
+    ref, _ = pm_amd.render(gs, cam, cfg.width, cfg.height, cfg.spp, cfg.depth, cfg.sky, lights, gmap, cmap,
+                           want_rgb=False)
+    be = pmdist.GpuBackend(gs, lights, cfg, 0, 1)
+    rgba = torch.zeros((cfg.height, cfg.width), dtype=torch.int32, device="cuda")
+    for _ in range(2):
+        rgba.zero_()
+        out, info = pmdist.frame(be, 0, 1, None, rgba)
+        assert info["n_global"] == gmap.n and info["n_caustic"] == cmap.n
+        assert torch.equal(out, ref)
