@@ -215,6 +215,8 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths
         O.cvalid[v] = 0;
 #pragma unroll 1
         for (int j = 0; j < kNumDiffuseSamples; j++) O.gvalid[(int64_t)v * kNumDiffuseSamples + j] = 0;
+        // no shadow rays from a miss (k_shadow_rays / k_direct skip w < 0)
+        for (int l = 0; l < A.nl; l++) O.sray[v * A.nl + l] = make_float4(0.f, 0.f, 0.f, -1.f);
       } else {
         const v3 albedo = {hr.m0.x, hr.m0.y, hr.m0.z};
         const float diffuse_brdf = hr.m0.w / kPI;
