@@ -391,6 +391,22 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
   return h;
 }
 
+// 30-bit Morton code of a point inside the box (lo, 1 / extent): only used to
+// order work for locality, never for a result.
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+__device__ __forceinline__ uint32_t morton30(float x, float y, float z, float3 lo, float3 inv) {
+  const float fx = fminf(fmaxf((x - lo.x) * inv.x * 1024.0f, 0.0f), 1023.0f);
+  const float fy = fminf(fmaxf((y - lo.y) * inv.y * 1024.0f, 0.0f), 1023.0f);
+  const float fz = fminf(fmaxf((z - lo.z) * inv.z * 1024.0f, 0.0f), 1023.0f);
+  return (spread3((uint32_t)fx) << 2) | (spread3((uint32_t)fy) << 1) | spread3((uint32_t)fz);
+}
+
 // The %.6f text round trip of the two-process pipeline (writeAlivePhotons,
 // photon-mapping/src/hostCode.cu:31-49 -> readPhotonsFromFile, ray-tracer/src/
 // hostCode.cu:26-52) without the text: printf rounds the exact value to 6

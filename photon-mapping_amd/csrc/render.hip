@@ -354,23 +354,12 @@ __global__ void k_compact_q(const float4* q, const uint32_t* valid, const uint32
   if (valid[i]) dense[idx[i]] = q[i];
 }
 
-__device__ __forceinline__ uint32_t spread3(uint32_t v) {
-  v = (v * 0x00010001u) & 0xFF0000FFu;
-  v = (v * 0x00000101u) & 0x0F00F00Fu;
-  v = (v * 0x00000011u) & 0xC30C30C3u;
-  v = (v * 0x00000005u) & 0x49249249u;
-  return v;
-}
-
 // 30-bit Morton code of each query position (scene bounds) + identity permutation
 __global__ void k_query_morton(const float4* q, int64_t n, float3 lo, float3 inv, uint32_t* keys, uint32_t* perm) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float4 p = q[i];
-  const float fx = fminf(fmaxf((p.x - lo.x) * inv.x * 1024.0f, 0.0f), 1023.0f);
-  const float fy = fminf(fmaxf((p.y - lo.y) * inv.y * 1024.0f, 0.0f), 1023.0f);
-  const float fz = fminf(fmaxf((p.z - lo.z) * inv.z * 1024.0f, 0.0f), 1023.0f);
-  keys[i] = (spread3((uint32_t)fx) << 2) | (spread3((uint32_t)fy) << 1) | spread3((uint32_t)fz);
+  keys[i] = morton30(p.x, p.y, p.z, lo, inv);
   perm[i] = (uint32_t)i;
 }
 __global__ void k_permute_q(const float4* src, const uint32_t* perm, int64_t n, float4* dst) {

@@ -10,6 +10,7 @@
 // deterministic slots: deposit k of photon i lands in slots[k][i] (coalesced
 // across the wave), then a scan + compaction writes the canonical
 // (g, bounce) order.
+#include <algorithm>
 #include <cstdlib>
 #include <utility>
 
@@ -242,6 +243,31 @@ __global__ __launch_bounds__(256) void k_ph_shade(DevScene S, const PhotonRay* _
   if (keep) out[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = nr;
 }
 
+// Bounce rays reordered by the Morton code of their origin (PM_TRACE_SORT,
+// default on): neighbouring lanes then start in the same BVH region. The order
+// of rays never changes a result (deposits go to slots[n][photon]).
+// key = top `mbits` of the origin's Morton code, then (dir3) the direction octant
+__global__ void k_ray_morton(const PhotonRay* __restrict__ rays, int64_t n, float3 lo, float3 inv, int mbits,
+                             int dir3, uint32_t* __restrict__ keys, uint32_t* __restrict__ perm) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 o = rays[i].o;
+  uint32_t k = morton30(o.x, o.y, o.z, lo, inv) >> (30 - mbits);
+  if (dir3) {
+    const float4 d = rays[i].d;
+    k = (k << 3) | (d.x < 0.f ? 4u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 1u : 0u);
+  }
+  keys[i] = k;
+  perm[i] = (uint32_t)i;
+}
+
+__global__ void k_ray_permute(const PhotonRay* __restrict__ src, const uint32_t* __restrict__ perm, int64_t n,
+                              PhotonRay* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dst[i] = src[perm[i]];
+}
+
 hipError_t launch_trace_wavefront(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl,
                                   int64_t g_lo, int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt,
                                   hipStream_t s) {
@@ -254,6 +280,24 @@ hipError_t launch_trace_wavefront(pm_scene* sc, const LightDev* d_lights, const 
   PM_HIP_TRY(hipMemcpyAsync(counts.p, &n0, sizeof(uint32_t), hipMemcpyHostToDevice, s));
   k_ph_gen<<<grid_for(np, 256), 256, 0, s>>>(d_lights, d_loff, nl, g_lo, np, ra.p);
   PM_HIP_TRY(hipGetLastError());
+  const char* senv = std::getenv("PM_TRACE_SORT");
+  const bool sort_rays = !senv || std::atoi(senv) != 0;
+  const char* benv = std::getenv("PM_TRACE_SORT_BITS");
+  // config 3 (trace ms): unsorted 57.8, 30 bits 55.6, 24 bits 54.9, 16 bits 54.6 (two radix passes),
+  // 21 bits + direction octant 54.6
+  const int mbits = benv ? std::min(30, std::max(3, std::atoi(benv))) : 16;
+  const char* denv = std::getenv("PM_TRACE_SORT_DIR");
+  const int dir3 = denv && std::atoi(denv) != 0 ? 1 : 0;
+  DevBuf<uint32_t> keys, perm;
+  if (sort_rays) {
+    keys.alloc(np);
+    perm.alloc(np);
+    if (!keys.p || !perm.p) return hipErrorOutOfMemory;
+  }
+  const pm_box& bb = sc->bounds;
+  const float3 lo = make_float3(bb.lower.x, bb.lower.y, bb.lower.z);
+  const float ex = bb.upper.x - bb.lower.x, ey = bb.upper.y - bb.lower.y, ez = bb.upper.z - bb.lower.z;
+  const float3 inv = make_float3(ex > 0.f ? 1.0f / ex : 0.f, ey > 0.f ? 1.0f / ey : 0.f, ez > 0.f ? 1.0f / ez : 0.f);
   PhotonRay *cur = ra.p, *nxt = rb.p;
   for (int b = 0; b < maxd; b++) {
     // grids sized for np: lanes past the live count exit at once
@@ -262,7 +306,20 @@ hipError_t launch_trace_wavefront(pm_scene* sc, const LightDev* d_lights, const 
     k_ph_shade<<<grid_for(np, 256), 256, 0, s>>>(sc->view(), cur, counts.p + b, hits.p, nxt, counts.p + b + 1, np,
                                                  maxd, caustic, slots, cnt);
     PM_HIP_TRY(hipGetLastError());
-    std::swap(cur, nxt);
+    if (sort_rays && b + 1 < maxd) {
+      uint32_t live = 0;
+      PM_HIP_TRY(hipMemcpyAsync(&live, counts.p + b + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      PM_HIP_TRY(hipStreamSynchronize(s));
+      if (live == 0) break;
+      k_ray_morton<<<grid_for(live, 256), 256, 0, s>>>(nxt, live, lo, inv, mbits, dir3, keys.p, perm.p);
+      PM_HIP_TRY(hipGetLastError());
+      PM_HIP_TRY(radix_sort_pairs(keys.p, perm.p, live, mbits + 3 * dir3, s));
+      // the input rays of this bounce are dead: sorted rays go there
+      k_ray_permute<<<grid_for(live, 256), 256, 0, s>>>(nxt, perm.p, live, cur);
+      PM_HIP_TRY(hipGetLastError());
+    } else {
+      std::swap(cur, nxt);
+    }
   }
   // keep the scratch alive until the stream has consumed it (DevBuf frees on scope exit)
   return hipStreamSynchronize(s);
