@@ -147,12 +147,11 @@ __global__ __launch_bounds__(256) void k_ph_gen(const LightDev* __restrict__ lig
   rays[i] = r;
 }
 
-__global__ __launch_bounds__(kTBlock) void k_ph_trace(DevScene S, const PhotonRay* __restrict__ rays,
-                                                      const uint32_t* __restrict__ count, float2* __restrict__ hits,
-                                                      int* overflow) {
+__global__ __launch_bounds__(kTBlock) void k_ph_trace(DevScene S, const PhotonRay* __restrict__ rays, int64_t n,
+                                                      float2* __restrict__ hits, int* overflow) {
   __shared__ int stack[kStackDepth * kTBlock];
   const int64_t i = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
-  if (i >= *count) return;
+  if (i >= n) return;
   const float4 o = rays[i].o, d = rays[i].d;
   Ray r;
   ray_prep(r, v3{o.x, o.y, o.z}, v3{d.x, d.y, d.z});
@@ -160,16 +159,25 @@ __global__ __launch_bounds__(kTBlock) void k_ph_trace(DevScene S, const PhotonRa
   hits[i] = make_float2(h.t, __int_as_float(h.slot));
 }
 
-__global__ __launch_bounds__(256) void k_ph_shade(DevScene S, const PhotonRay* __restrict__ in,
-                                                  const uint32_t* __restrict__ count_in,
-                                                  const float2* __restrict__ hits, PhotonRay* __restrict__ out,
-                                                  uint32_t* __restrict__ count_out, int64_t np, int maxd,
-                                                  int caustic, pm_photon* __restrict__ slots,
-                                                  uint32_t* __restrict__ cnt) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Surviving rays are appended with ONE atomic per 1024-thread block (a
+// same-address atomic per wave serialised at one L2 channel: ~2/3 of the
+// kernel). With `keys`, the next bounce's sort key (top `mbits` of the origin's
+// Morton code) is written beside the ray.
+constexpr int kShadeBlock = 1024;
+
+__global__ __launch_bounds__(kShadeBlock) void k_ph_shade(DevScene S, const PhotonRay* __restrict__ in,
+                                                          int64_t n_in, const float2* __restrict__ hits,
+                                                          PhotonRay* __restrict__ out,
+                                                          uint32_t* __restrict__ count_out, int64_t np, int maxd,
+                                                          int caustic, pm_photon* __restrict__ slots,
+                                                          uint32_t* __restrict__ cnt, uint32_t* __restrict__ keys,
+                                                          float3 klo, float3 kinv, int mbits) {
+  __shared__ uint32_t wcount[kShadeBlock / 64];
+  __shared__ uint32_t block_base;
+  const int64_t i = (int64_t)blockIdx.x * kShadeBlock + threadIdx.x;
   bool keep = false;
   PhotonRay nr;
-  if (i < *count_in) {
+  if (i < n_in) {
     const PhotonRay pr = in[i];
     const float2 hh = hits[i];
     const int slot = __float_as_int(hh.y);
@@ -232,33 +240,32 @@ __global__ __launch_bounds__(256) void k_ph_shade(DevScene S, const PhotonRay* _
       nr.c = make_float4(sc.x, sc.y, sc.z, __uint_as_float((n << 8) | (uint32_t)(b + 1)));
     }
   }
-  // wave-aggregated append
+  // block-aggregated append
   const uint64_t m = __ballot(keep);
-  if (m == 0) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)m) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(count_out, (uint32_t)__popcll(m));
-  base = (uint32_t)__shfl((int)base, leader);
-  if (keep) out[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = nr;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) wcount[wave] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kShadeBlock / 64; w++) tot += wcount[w];
+    block_base = tot ? atomicAdd(count_out, tot) : 0u;
+  }
+  __syncthreads();
+  if (!keep) return;
+  uint32_t off = block_base;
+  for (int w = 0; w < wave; w++) off += wcount[w];
+  const uint32_t dst = off + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+  out[dst] = nr;
+  if (keys) keys[dst] = morton30(nr.o.x, nr.o.y, nr.o.z, klo, kinv) >> (30 - mbits);
 }
 
 // Bounce rays reordered by the Morton code of their origin (PM_TRACE_SORT,
 // default on): neighbouring lanes then start in the same BVH region. The order
 // of rays never changes a result (deposits go to slots[n][photon]).
-// key = top `mbits` of the origin's Morton code, then (dir3) the direction octant
-__global__ void k_ray_morton(const PhotonRay* __restrict__ rays, int64_t n, float3 lo, float3 inv, int mbits,
-                             int dir3, uint32_t* __restrict__ keys, uint32_t* __restrict__ perm) {
+__global__ void k_iota(uint32_t* __restrict__ perm, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float4 o = rays[i].o;
-  uint32_t k = morton30(o.x, o.y, o.z, lo, inv) >> (30 - mbits);
-  if (dir3) {
-    const float4 d = rays[i].d;
-    k = (k << 3) | (d.x < 0.f ? 4u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 1u : 0u);
-  }
-  keys[i] = k;
-  perm[i] = (uint32_t)i;
+  if (i < n) perm[i] = (uint32_t)i;
 }
 
 __global__ void k_ray_permute(const PhotonRay* __restrict__ src, const uint32_t* __restrict__ perm, int64_t n,
@@ -271,24 +278,16 @@ __global__ void k_ray_permute(const PhotonRay* __restrict__ src, const uint32_t*
 hipError_t launch_trace_wavefront(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl,
                                   int64_t g_lo, int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt,
                                   hipStream_t s) {
-  DevBuf<PhotonRay> ra(np), rb(np);
-  DevBuf<float2> hits(np);
-  DevBuf<uint32_t> counts(maxd + 1);
-  if (!ra.p || !rb.p || !hits.p || !counts.p) return hipErrorOutOfMemory;
-  PM_HIP_TRY(hipMemsetAsync(counts.p, 0, sizeof(uint32_t) * (maxd + 1), s));
-  const uint32_t n0 = (uint32_t)np;
-  PM_HIP_TRY(hipMemcpyAsync(counts.p, &n0, sizeof(uint32_t), hipMemcpyHostToDevice, s));
-  k_ph_gen<<<grid_for(np, 256), 256, 0, s>>>(d_lights, d_loff, nl, g_lo, np, ra.p);
-  PM_HIP_TRY(hipGetLastError());
   const char* senv = std::getenv("PM_TRACE_SORT");
   const bool sort_rays = !senv || std::atoi(senv) != 0;
-  const char* benv = std::getenv("PM_TRACE_SORT_BITS");
   // config 3 (trace ms): unsorted 57.8, 30 bits 55.6, 24 bits 54.9, 16 bits 54.6 (two radix passes),
   // 21 bits + direction octant 54.6
-  const int mbits = benv ? std::min(30, std::max(3, std::atoi(benv))) : 16;
-  const char* denv = std::getenv("PM_TRACE_SORT_DIR");
-  const int dir3 = denv && std::atoi(denv) != 0 ? 1 : 0;
-  DevBuf<uint32_t> keys, perm;
+  const char* benv = std::getenv("PM_TRACE_SORT_BITS");
+  const int mbits = benv ? std::min(30, std::max(8, std::atoi(benv))) : 16;
+  DevBuf<PhotonRay> ra(np), rb(np);
+  DevBuf<float2> hits(np);
+  DevBuf<uint32_t> counts(1), keys, perm;
+  if (!ra.p || !rb.p || !hits.p || !counts.p) return hipErrorOutOfMemory;
   if (sort_rays) {
     keys.alloc(np);
     perm.alloc(np);
@@ -298,22 +297,29 @@ hipError_t launch_trace_wavefront(pm_scene* sc, const LightDev* d_lights, const 
   const float3 lo = make_float3(bb.lower.x, bb.lower.y, bb.lower.z);
   const float ex = bb.upper.x - bb.lower.x, ey = bb.upper.y - bb.lower.y, ez = bb.upper.z - bb.lower.z;
   const float3 inv = make_float3(ex > 0.f ? 1.0f / ex : 0.f, ey > 0.f ? 1.0f / ey : 0.f, ez > 0.f ? 1.0f / ez : 0.f);
+  k_ph_gen<<<grid_for(np, 256), 256, 0, s>>>(d_lights, d_loff, nl, g_lo, np, ra.p);
+  PM_HIP_TRY(hipGetLastError());
   PhotonRay *cur = ra.p, *nxt = rb.p;
-  for (int b = 0; b < maxd; b++) {
-    // grids sized for np: lanes past the live count exit at once
-    k_ph_trace<<<grid_for(np, kTBlock), kTBlock, 0, s>>>(sc->view(), cur, counts.p + b, hits.p, sc->overflow.p);
+  int64_t live = np;
+  for (int b = 0; b < maxd && live > 0; b++) {
+    const bool last = b + 1 >= maxd;
+    const bool sort_next = sort_rays && !last;
+    PM_HIP_TRY(hipMemsetAsync(counts.p, 0, sizeof(uint32_t), s));
+    k_ph_trace<<<grid_for(live, kTBlock), kTBlock, 0, s>>>(sc->view(), cur, live, hits.p, sc->overflow.p);
     PM_HIP_TRY(hipGetLastError());
-    k_ph_shade<<<grid_for(np, 256), 256, 0, s>>>(sc->view(), cur, counts.p + b, hits.p, nxt, counts.p + b + 1, np,
-                                                 maxd, caustic, slots, cnt);
+    k_ph_shade<<<grid_for(live, kShadeBlock), kShadeBlock, 0, s>>>(sc->view(), cur, live, hits.p, nxt, counts.p, np,
+                                                                   maxd, caustic, slots, cnt,
+                                                                   sort_next ? keys.p : nullptr, lo, inv, mbits);
     PM_HIP_TRY(hipGetLastError());
-    if (sort_rays && b + 1 < maxd) {
-      uint32_t live = 0;
-      PM_HIP_TRY(hipMemcpyAsync(&live, counts.p + b + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-      PM_HIP_TRY(hipStreamSynchronize(s));
-      if (live == 0) break;
-      k_ray_morton<<<grid_for(live, 256), 256, 0, s>>>(nxt, live, lo, inv, mbits, dir3, keys.p, perm.p);
+    if (last) break;
+    uint32_t nl_host = 0;
+    PM_HIP_TRY(hipMemcpyAsync(&nl_host, counts.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    live = nl_host;
+    if (sort_next && live > 1) {
+      k_iota<<<grid_for(live, 256), 256, 0, s>>>(perm.p, live);
       PM_HIP_TRY(hipGetLastError());
-      PM_HIP_TRY(radix_sort_pairs(keys.p, perm.p, live, mbits + 3 * dir3, s));
+      PM_HIP_TRY(radix_sort_pairs(keys.p, perm.p, live, mbits, s));
       // the input rays of this bounce are dead: sorted rays go there
       k_ray_permute<<<grid_for(live, 256), 256, 0, s>>>(nxt, perm.p, live, cur);
       PM_HIP_TRY(hipGetLastError());

@@ -2,8 +2,7 @@
 # A/B of the bounce-ray sort knobs on config 3 (run on the GPU box from the repo root).
 set -e
 mkdir -p gpurun_out/tsort
-for v in "PM_TRACE_SORT=0" "PM_TRACE_SORT_BITS=30" "PM_TRACE_SORT_BITS=24" "PM_TRACE_SORT_BITS=16" \
-         "PM_TRACE_SORT_BITS=21 PM_TRACE_SORT_DIR=1" "PM_TRACE_SORT_BITS=13 PM_TRACE_SORT_DIR=1"; do
+for v in "PM_TRACE_SORT=0" "PM_TRACE_SORT_BITS=24" "PM_TRACE_SORT_BITS=16" "PM_TRACE_SORT_BITS=12"; do
   env $v timeout -k 10 200 python bench.py --no-cpu-baseline --steps 3 > gpurun_out/tsort/b.log 2>&1
   python - "$v" <<'PY'
 import json, sys
