@@ -11,7 +11,7 @@
 // active subtree range at its left-balanced median — the median element is read
 // directly from the list of the chosen dimension and the three lists are
 // stably partitioned around it (segmented count scan over 1024-position tiles:
-// k_kd_count -> k_kd_tilescan -> k_kd_part). Subtree ranges are identical in the three lists, so a single tag
+// k_kd_count -> k_kd_chunkscan / k_kd_chunkcarry -> k_kd_part). Subtree ranges are identical in the three lists, so a single tag
 // array tracks subtree membership. Ties are broken by the original index.
 #include <algorithm>
 #include <cstdlib>
@@ -106,7 +106,7 @@ __device__ __forceinline__ int kd_class(const float4 e, int dim, float nc, int n
 // classed against its segment's median (L / M / R / already placed) and the
 // packed (L, R) counts are scanned SEGMENTED (reset at segment starts):
 //   k_kd_count     per-tile segmented aggregate,
-//   k_kd_tilescan  one block: exclusive segmented carry per tile,
+//   k_kd_chunkscan / k_kd_chunkcarry  exclusive segmented carry per tile,
 //   k_kd_part      block scan + carry -> stable scatter: L -> b + #L before it
 //                  in the segment, M -> b + ls, R -> b + ls + 1 + #R before it;
 //                  the tag (segment id per position) is updated in place.
@@ -235,28 +235,37 @@ __global__ __launch_bounds__(kPartThreads) void k_kd_count(const float4* __restr
   if (threadIdx.x == 0) tile_agg[blockIdx.x] = agg;
 }
 
-// One block: exclusive segmented prefix over the tile aggregates.
-constexpr int kTileScanThreads = 1024;
-__global__ __launch_bounds__(kTileScanThreads) void k_kd_tilescan(const SegVal* __restrict__ agg, int64_t ntiles,
-                                                                  SegVal* __restrict__ carry) {
-  __shared__ SegVal sh[kTileScanThreads / 64];
-  const int64_t per = (ntiles + kTileScanThreads - 1) / kTileScanThreads;
-  const int64_t t0 = (int64_t)threadIdx.x * per, t1 = min(ntiles, t0 + per);
-  SegVal th = seg_zero();
-  for (int64_t t = t0; t < t1; t++) th = seg_combine(th, agg[t]);
+// Exclusive segmented prefix over the tile aggregates in two coalesced steps:
+// k_kd_chunkscan scans chunks of 1024 tiles (one block each) and records each
+// chunk's total; k_kd_chunkcarry scans the chunk totals in place (one block,
+// <= 1024 chunks, i.e. < 2^30 positions). k_kd_part combines the two carries.
+// (A single block walking all tiles cost ~115 us per level.)
+constexpr int kChunk = 1024;
+__global__ __launch_bounds__(kChunk) void k_kd_chunkscan(const SegVal* __restrict__ agg, int64_t ntiles,
+                                                         SegVal* __restrict__ carry, SegVal* __restrict__ chunk_agg) {
+  __shared__ SegVal sh[kChunk / 64];
+  const int64_t t = (int64_t)blockIdx.x * kChunk + threadIdx.x;
+  const SegVal v = t < ntiles ? agg[t] : seg_zero();
   SegVal total;
-  SegVal run = block_seg_scan<kTileScanThreads / 64>(th, sh, total);
-  for (int64_t t = t0; t < t1; t++) {
-    carry[t] = run;
-    run = seg_combine(run, agg[t]);
-  }
+  const SegVal ex = block_seg_scan<kChunk / 64>(v, sh, total);
+  if (t < ntiles) carry[t] = ex;
+  if (threadIdx.x == 0) chunk_agg[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kChunk) void k_kd_chunkcarry(SegVal* __restrict__ chunk_agg, int nchunks) {
+  __shared__ SegVal sh[kChunk / 64];
+  const SegVal v = (int)threadIdx.x < nchunks ? chunk_agg[threadIdx.x] : seg_zero();
+  SegVal total;
+  const SegVal ex = block_seg_scan<kChunk / 64>(v, sh, total);   // every read precedes its barriers
+  if ((int)threadIdx.x < nchunks) chunk_agg[threadIdx.x] = ex;
 }
 
 __global__ __launch_bounds__(kPartThreads) void k_kd_part(const float4* __restrict__ l0, const float4* __restrict__ l1,
                                                           const float4* __restrict__ l2, float4* __restrict__ o0,
                                                           float4* __restrict__ o1, float4* __restrict__ o2,
                                                           int32_t* __restrict__ tag, int64_t n, SegTab T,
-                                                          const SegVal* __restrict__ tile_carry) {
+                                                          const SegVal* __restrict__ tile_carry,
+                                                          const SegVal* __restrict__ chunk_carry) {
   __shared__ SegVal sh[kPartThreads / 64];
   const int64_t base = (int64_t)blockIdx.x * kPartTile + threadIdx.x;
   float4* O[3] = {o0, o1, o2};
@@ -266,7 +275,7 @@ __global__ __launch_bounds__(kPartThreads) void k_kd_part(const float4* __restri
 #pragma unroll
   for (int k = 0; k < kPartIPT; k++)
     th[k] = part_load<true>(l0, l1, l2, tag, n, T, base + k * kPartThreads, it[k], e[k]);
-  SegVal carry = tile_carry[blockIdx.x];
+  SegVal carry = seg_combine(chunk_carry[blockIdx.x / kChunk], tile_carry[blockIdx.x]);
 #pragma unroll
   for (int k = 0; k < kPartIPT; k++) {
     SegVal total;
@@ -424,8 +433,9 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
   DevBuf<int32_t> tb(cap), ts(cap), tls(cap), tdim(cap), tid(cap), tag(n);
   DevBuf<float> tco(cap);
   const int64_t ntiles = (n + kPartTile - 1) / kPartTile;
-  DevBuf<SegVal> tagg(ntiles), tcarry(ntiles);
-  if (!tb.p || !ts.p || !tls.p || !tdim.p || !tid.p || !tag.p || !tco.p || !tagg.p || !tcarry.p)
+  const int nchunks = (int)((ntiles + kChunk - 1) / kChunk);
+  DevBuf<SegVal> tagg(ntiles), tcarry(ntiles), ccarry(nchunks);
+  if (!tb.p || !ts.p || !tls.p || !tdim.p || !tid.p || !tag.p || !tco.p || !tagg.p || !tcarry.p || !ccarry.p)
     return hipErrorOutOfMemory;
   SegTab T{tb.p, ts.p, tls.p, tdim.p, tco.p, tid.p};
   const int32_t root[2] = {0, (int32_t)n};
@@ -450,10 +460,12 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
     if (L == H - 1) break;   // last level: every remaining subtree has one node
     k_kd_count<<<(int)ntiles, kPartThreads, 0, s>>>(cur[0], cur[1], cur[2], tag.p, n, T, tagg.p);
     PM_HIP_TRY(hipGetLastError());
-    k_kd_tilescan<<<1, kTileScanThreads, 0, s>>>(tagg.p, ntiles, tcarry.p);
+    k_kd_chunkscan<<<nchunks, kChunk, 0, s>>>(tagg.p, ntiles, tcarry.p, ccarry.p);
+    PM_HIP_TRY(hipGetLastError());
+    k_kd_chunkcarry<<<1, kChunk, 0, s>>>(ccarry.p, nchunks);
     PM_HIP_TRY(hipGetLastError());
     k_kd_part<<<(int)ntiles, kPartThreads, 0, s>>>(cur[0], cur[1], cur[2], nxt[0], nxt[1], nxt[2], tag.p, n, T,
-                                                   tcarry.p);
+                                                   tcarry.p, ccarry.p);
     PM_HIP_TRY(hipGetLastError());
     for (int d = 0; d < 3; d++) {
       float4* t = cur[d];
@@ -506,15 +518,31 @@ __global__ void k_map_export(const float4* nodes, const float4* payload, int64_t
   out[t] = p;
 }
 
+// wave-reduced first: one atomic per wave and component (same-address global
+// atomics serialise at one L2 channel)
 __global__ void k_bounds(const float4* elems, int64_t n, unsigned* ob) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float4 e = elems[i];
-  const float c[3] = {e.x, e.y, e.z};
+  uint32_t mn[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, mx[3] = {0u, 0u, 0u};
+  if (i < n) {
+    const float4 e = elems[i];
+    const float c[3] = {e.x, e.y, e.z};
+#pragma unroll
+    for (int k = 0; k < 3; k++) mn[k] = mx[k] = orderable_key(c[k]);
+  }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    atomicMin(&ob[k], orderable_key(c[k]));
-    atomicMax(&ob[3 + k], orderable_key(c[k]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mn[k] = min(mn[k], (uint32_t)__shfl_xor((int)mn[k], o));
+      mx[k] = max(mx[k], (uint32_t)__shfl_xor((int)mx[k], o));
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      atomicMin(&ob[k], mn[k]);
+      atomicMax(&ob[3 + k], mx[k]);
+    }
   }
 }
 

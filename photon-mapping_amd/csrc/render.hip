@@ -192,89 +192,94 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths
   __shared__ int stack[kStackDepth * kRBlock];
   const int64_t tid = (int64_t)blockIdx.x * kRBlock + threadIdx.x;
   int px, py;
-  if (!pixel_of(A, tid, px, py)) return;
-  int* st = stack + threadIdx.x;
-  uint32_t rng = lcg_init((uint32_t)px, (uint32_t)py);
-  HitRec hr;
-  hr.hitpoint = hr.normal = {0.f, 0.f, 0.f};
-  hr.m0 = hr.m1 = make_float4(0.f, 0.f, 0.f, 0.f);
-  int64_t v = voff[tid];
+  const bool valid = pixel_of(A, tid, px, py);
   uint32_t nrays = 0;
-  for (int s = 0; s < A.spp; s++) {
-    v3 ro = A.cam_pos;
-    v3 rd = camera_dir(A, px, py, rng);
-    v3 att = {1.f, 1.f, 1.f};
-    for (int d = 0; d < A.depth; d++, v++) {
-      nrays++;
-      const bool hit = trace_closest(S, ro, rd, kEPS, kINFTY, hr, st, overflow);
-      O.vatt[v] = make_float4(att.x, att.y, att.z, 0.f);
-      uint32_t fl = 0;
-      if (!hit) {
-        fl |= VF_MISS;
-        O.vdirect[v] = make_float4(A.sky.x, A.sky.y, A.sky.z, 0.f);
-        O.cvalid[v] = 0;
-#pragma unroll 1
-        for (int j = 0; j < kNumDiffuseSamples; j++) O.gvalid[(int64_t)v * kNumDiffuseSamples + j] = 0;
-        // no shadow rays from a miss (k_shadow_rays / k_direct skip w < 0)
-        for (int l = 0; l < A.nl; l++) O.sray[v * A.nl + l] = make_float4(0.f, 0.f, 0.f, -1.f);
-      } else {
-        const v3 albedo = {hr.m0.x, hr.m0.y, hr.m0.z};
-        const float diffuse_brdf = hr.m0.w / kPI;
-        // direct light (deviceCode.cu:145-171): the shadow rays are cast by
-        // k_shadow_rays; the per-light term is kept so that k_direct sums it
-        // in the reference's order with the visibility
-        for (int l = 0; l < A.nl; l++) {
-          const LightR L = A.lights[l];
-          const v3 org = hr.hitpoint;
-          v3 ldir = sub(v3{L.pos.x, L.pos.y, L.pos.z}, org);
-          const float dist = norm3(ldir);
-          ldir = normalize(ldir);
-          const float ldn = dot(ldir, hr.normal);
-          const int64_t si = v * A.nl + l;
-          if (ldn < 0.f) {
-            O.sray[si] = make_float4(0.f, 0.f, 0.f, -1.f);
-            continue;
-          }
-          nrays++;
-          // specularBrdf (shading.h:82-91)
-          const float sb = near_zero(sub(reflect(ldir, hr.normal), rd)) ? hr.m1.x : 0.f;
-          const float inv = 1.f / (dist * dist);
-          O.sray[si] = make_float4(ldir.x, ldir.y, ldir.z, dist * (1.f - kEPS));
-          O.sterm[si] = make_float4(ldn, inv, diffuse_brdf + sb, 0.f);
-        }
-        O.valb[v] = make_float4(albedo.x, albedo.y, albedo.z, 0.f);
-        O.cq[v] = make_float4(hr.hitpoint.x, hr.hitpoint.y, hr.hitpoint.z, diffuse_brdf);
-        O.cvalid[v] = 1;
-        // the 20 final-gather rays (deviceCode.cu:112-131): directions here (RNG
-        // order unchanged), traversal in k_diffuse_rays
-        for (int j = 0; j < kNumDiffuseSamples; j++) {
-          const int64_t gi = (int64_t)v * kNumDiffuseSamples + j;
-          uint32_t cast = 0;
-          if (diffuse_brdf > 0.f) {
-            const v3 rdir = diffuse_direction(hr.normal, rng);
-            O.gdir[gi] = make_float4(rdir.x, rdir.y, rdir.z, 0.f);
+  if (valid) {
+    int* st = stack + threadIdx.x;
+    uint32_t rng = lcg_init((uint32_t)px, (uint32_t)py);
+    HitRec hr;
+    hr.hitpoint = hr.normal = {0.f, 0.f, 0.f};
+    hr.m0 = hr.m1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t v = voff[tid];
+    for (int s = 0; s < A.spp; s++) {
+      v3 ro = A.cam_pos;
+      v3 rd = camera_dir(A, px, py, rng);
+      v3 att = {1.f, 1.f, 1.f};
+      for (int d = 0; d < A.depth; d++, v++) {
+        nrays++;
+        const bool hit = trace_closest(S, ro, rd, kEPS, kINFTY, hr, st, overflow);
+        O.vatt[v] = make_float4(att.x, att.y, att.z, 0.f);
+        uint32_t fl = 0;
+        if (!hit) {
+          fl |= VF_MISS;
+          O.vdirect[v] = make_float4(A.sky.x, A.sky.y, A.sky.z, 0.f);
+          O.cvalid[v] = 0;
+  #pragma unroll 1
+          for (int j = 0; j < kNumDiffuseSamples; j++) O.gvalid[(int64_t)v * kNumDiffuseSamples + j] = 0;
+          // no shadow rays from a miss (k_shadow_rays / k_direct skip w < 0)
+          for (int l = 0; l < A.nl; l++) O.sray[v * A.nl + l] = make_float4(0.f, 0.f, 0.f, -1.f);
+        } else {
+          const v3 albedo = {hr.m0.x, hr.m0.y, hr.m0.z};
+          const float diffuse_brdf = hr.m0.w / kPI;
+          // direct light (deviceCode.cu:145-171): the shadow rays are cast by
+          // k_shadow_rays; the per-light term is kept so that k_direct sums it
+          // in the reference's order with the visibility
+          for (int l = 0; l < A.nl; l++) {
+            const LightR L = A.lights[l];
+            const v3 org = hr.hitpoint;
+            v3 ldir = sub(v3{L.pos.x, L.pos.y, L.pos.z}, org);
+            const float dist = norm3(ldir);
+            ldir = normalize(ldir);
+            const float ldn = dot(ldir, hr.normal);
+            const int64_t si = v * A.nl + l;
+            if (ldn < 0.f) {
+              O.sray[si] = make_float4(0.f, 0.f, 0.f, -1.f);
+              continue;
+            }
             nrays++;
-            cast = 1;
+            // specularBrdf (shading.h:82-91)
+            const float sb = near_zero(sub(reflect(ldir, hr.normal), rd)) ? hr.m1.x : 0.f;
+            const float inv = 1.f / (dist * dist);
+            O.sray[si] = make_float4(ldir.x, ldir.y, ldir.z, dist * (1.f - kEPS));
+            O.sterm[si] = make_float4(ldn, inv, diffuse_brdf + sb, 0.f);
           }
-          O.gvalid[gi] = cast;
+          O.valb[v] = make_float4(albedo.x, albedo.y, albedo.z, 0.f);
+          O.cq[v] = make_float4(hr.hitpoint.x, hr.hitpoint.y, hr.hitpoint.z, diffuse_brdf);
+          O.cvalid[v] = 1;
+          // the 20 final-gather rays (deviceCode.cu:112-131): directions here (RNG
+          // order unchanged), traversal in k_diffuse_rays
+          for (int j = 0; j < kNumDiffuseSamples; j++) {
+            const int64_t gi = (int64_t)v * kNumDiffuseSamples + j;
+            uint32_t cast = 0;
+            if (diffuse_brdf > 0.f) {
+              const v3 rdir = diffuse_direction(hr.normal, rng);
+              O.gdir[gi] = make_float4(rdir.x, rdir.y, rdir.z, 0.f);
+              nrays++;
+              cast = 1;
+            }
+            O.gvalid[gi] = cast;
+          }
         }
+        bool absorbed;
+        float coef;
+        const v3 od = reflect_or_refract(hr, rd, hr.normal, rng, absorbed, coef);
+        const bool last = absorbed || d == A.depth - 1;
+        if (last) fl |= VF_LAST;
+        O.vflags[v] = fl;
+        if (absorbed) {
+          v++;
+          break;
+        }
+        att = mulv(att, smul(coef, v3{hr.m0.x, hr.m0.y, hr.m0.z}));
+        ro = hr.hitpoint;
+        rd = od;
       }
-      bool absorbed;
-      float coef;
-      const v3 od = reflect_or_refract(hr, rd, hr.normal, rng, absorbed, coef);
-      const bool last = absorbed || d == A.depth - 1;
-      if (last) fl |= VF_LAST;
-      O.vflags[v] = fl;
-      if (absorbed) {
-        v++;
-        break;
-      }
-      att = mulv(att, smul(coef, v3{hr.m0.x, hr.m0.y, hr.m0.z}));
-      ro = hr.hitpoint;
-      rd = od;
     }
   }
-  atomicAdd(O.rays, (unsigned long long)nrays);
+  // one atomic per wave (every lane reaches here; lanes outside the image add 0)
+  unsigned long long nr = nrays;
+  for (int o = 32; o > 0; o >>= 1) nr += (unsigned long long)__shfl_xor((long long)nr, o);
+  if ((threadIdx.x & 63) == 0 && nr) atomicAdd(O.rays, nr);
 }
 
 // Final-gather rays: closest hit from the vertex; a hit with a diffuse
