@@ -202,9 +202,13 @@ __device__ __forceinline__ SegVal part_load(const float4* __restrict__ l0, const
   th.f = it.tg >= 0 && p == it.sb;
 #pragma unroll
   for (int d = 0; d < 3; d++) {
-    const float4 x = p < n ? L[d][p] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // the segment's own split-dimension list is sorted on that dimension, so
+    // its classes are positional: the count pass does not load it
+    const bool positional = it.tg >= 0 && d == dim;
+    const float4 x = (p < n && (KEEP || !positional)) ? L[d][p] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (KEEP) e[d] = x;
-    const int c = it.tg < 0 ? 3 : kd_class(x, dim, nc, nid);
+    const int64_t mid = (int64_t)it.sb + it.sls;
+    const int c = it.tg < 0 ? 3 : (positional ? (p < mid ? 0 : (p == mid ? 1 : 2)) : kd_class(x, dim, nc, nid));
     it.cls[d] = (uint8_t)c;
     th.v[d] = c == 0 ? 1ull : (c == 2 ? (1ull << 32) : 0ull);
   }
