@@ -197,6 +197,74 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
   }
 }
 
+// The gather's walk (PM_GATHER_MODE 11): knn_walk<K, POST = true, QL> with
+// fewer instructions per step, same visits and same result:
+//  - the cut-off d^2 < r2 lives in the sentinel, the largest key below
+//    (r2, id 0) (= (prev_float(r2), 0xFFFFFFFF)): `key < list[K-1]` alone
+//    admits exactly the candidates (no f32 / lo compares per step); the
+//    radius of a list that did not fill is r2 (radiance_r2);
+//  - the point test and the queue write are branch-free (a non-candidate is
+//    written above the queue top and overwritten later), finished lanes keep
+//    re-reading their last node and their results are masked, so the step
+//    runs without exec-mask branches; only the wave-uniform insert round
+//    branches.
+template <int K, int QL>
+__device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float r2, bool valid,
+                                              double (&list)[K], double* lq, int lstride) {
+  const double sentinel =
+      __longlong_as_double((long long)((((uint64_t)__float_as_uint(r2)) << 32) + kKeyBias - 1));
+#pragma unroll
+  for (int j = 0; j < K; j++) list[j] = sentinel;
+  if (n <= 0) return;   // empty map: every lane keeps the sentinel list (uniform)
+  float bound = key_d2(sentinel);
+  int prev = -1, curr = 0;
+  bool walking = valid;
+  int qn = 0;
+  for (;;) {
+    const float4 nd = nodes[curr];   // finished / invalid lanes re-read a valid node
+    const int child = 2 * curr + 1;
+    const int w = __float_as_int(nd.w);
+    const int dim = w & 3;
+    const float diff = (dim == 0 ? q.x : (dim == 1 ? q.y : q.z)) - (dim == 0 ? nd.x : (dim == 1 ? nd.y : nd.z));
+    const int side = diff > 0.f ? 1 : 0;
+    const int close_c = child + side, far_c = child + 1 - side;
+    const int parent = ((curr + 1) >> 1) - 1;
+    const bool down = prev < child;
+    const bool test = (down && close_c >= n) || prev == close_c;
+    const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
+    const float d2 = dx * dx + dy * dy + dz * dz;
+    const double key = key_make(d2, (uint32_t)(w >> 2));
+    const bool cand = walking && test && key < list[K - 1];
+    int next;
+    if (prev == far_c) next = parent;
+    else if (prev == close_c || close_c >= n) next = (far_c < n && diff * diff <= bound) ? far_c : parent;
+    else next = close_c;
+    lq[qn * lstride] = key;
+    qn += cand ? 1 : 0;
+    const bool go = walking && next >= 0;
+    prev = go ? curr : prev;
+    curr = go ? next : curr;
+    walking = go;
+    const bool any_walking = __ballot(walking) != 0;
+    if (__ballot(qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
+      const bool pop = qn > 0;
+      qn -= pop ? 1 : 0;
+      const double ik = pop ? lq[qn * lstride] : __longlong_as_double(0x7FEFFFFFFFFFFFFFll);
+      if (ik < list[K - 1]) {
+        list_insert<K>(list, ik);
+        bound = key_d2(list[K - 1]);
+      }
+      if (!any_walking && __ballot(qn > 0) == 0) break;
+    }
+  }
+}
+
+// radius^2 of a finished lean list: the K-th d^2, or r2 if the list did not fill
+template <int K>
+__device__ __forceinline__ float radiance_r2(const double (&list)[K], float r2) {
+  return key_id(list[K - 1]) == 0xFFFFFFFFu ? r2 : key_d2(list[K - 1]);
+}
+
 // pm_knn: K-wide list for k <= K; k > 128 runs 128-wide passes (j0 = output
 // offset of this pass, lo_in / lo_out = last key of the previous / this pass).
 template <int K, int QP>
@@ -226,8 +294,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 64 ? 4
 // Radiance estimate from a finished candidate list: gatherPhotons
 // (shading.h:93-121), neighbours summed in (d^2, index) order.
 __device__ __forceinline__ v3 radiance(const double (&list)[kKNearest], const float4* __restrict__ payload,
-                                       float brdf) {
-  const float r2 = key_d2(list[kKNearest - 1]);
+                                       float brdf, float r2) {
   v3 flux = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int p = 0; p < kKNearest; p++) {
@@ -242,7 +309,7 @@ __device__ __forceinline__ v3 radiance(const double (&list)[kKNearest], const fl
 }
 
 // TAG only separates the global-map launch into its own kernel symbol (rocprof).
-template <int TAG, bool POST, int QP, int QL = 0>
+template <int TAG, bool POST, int QP, int QL = 0, bool LEAN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out) {
@@ -254,10 +321,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool valid = i < nq;
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   double list[kKNearest];
-  knn_walk<kKNearest, POST, QP, false, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, kKMaxDistance * kKMaxDistance, valid,
-                                           list, nullptr, lq + threadIdx.x, 256);
+  const float R2 = kKMaxDistance * kKMaxDistance;
+  if (LEAN) {
+    knn_walk_lean<kKNearest, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, R2, valid, list, lq + threadIdx.x, 256);
+  } else {
+    knn_walk<kKNearest, POST, QP, false, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, R2, valid, list, nullptr,
+                                             lq + threadIdx.x, 256);
+  }
   if (valid) {
-    const v3 f = radiance(list, payload, qq.w);
+    const v3 f = radiance(list, payload, qq.w, LEAN ? radiance_r2(list, R2) : key_d2(list[kKNearest - 1]));
     out[i] = make_float4(f.x, f.y, f.z, 0.f);
   }
 }
@@ -361,26 +433,28 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
                          int tag) {
   if (nq <= 0) return hipSuccess;
   // A/B knob (read per launch), all variants return identical bits:
-  //   9 (default) post-order + 8-deep LDS insert queue        66.3 ms
+  //  11 (default) mode 9 with the lean step (knn_walk_lean)   62.3 ms
+  //   9 post-order + 8-deep LDS insert queue                  66.7 ms
   //   4 post-order, insert at once                             73.6 ms
   //   5 post-order + 4-entry VGPR queue (spills)               74.1 ms
   //  10 post-order + 16-deep LDS queue (staler bound)          69.1 ms
   //   0 pre-order, insert at once
   // (config 3 global map; depths 4 / 6: 67.3 / 66.4 ms)
   const char* env = std::getenv("PM_GATHER_MODE");
-  const int mode = env ? std::atoi(env) : 9;
+  const int mode = env ? std::atoi(env) : 11;
   if (std::getenv("PM_GATHER_STATS")) gather_stats(m, qb, nq, mode, s);
   const int g = grid_for(nq, 256);
   const int n = (int)m->n;
-#define PM_WALK(P, Q, L)                                                                                \
-  (tag == 1 ? (k_gather<1, P, Q, L><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out))          \
-            : (k_gather<0, P, Q, L><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out)))
+#define PM_WALK(P, Q, L, LEAN)                                                                          \
+  (tag == 1 ? (k_gather<1, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out))    \
+            : (k_gather<0, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out)))
   switch (mode) {
-    case 0: PM_WALK(false, 0, 0); break;
-    case 4: PM_WALK(true, 0, 0); break;
-    case 5: PM_WALK(true, 4, 0); break;
-    case 10: PM_WALK(true, 0, 16); break;
-    default: PM_WALK(true, 0, 8); break;
+    case 11: PM_WALK(true, 0, 8, true); break;
+    case 0: PM_WALK(false, 0, 0, false); break;
+    case 4: PM_WALK(true, 0, 0, false); break;
+    case 5: PM_WALK(true, 4, 0, false); break;
+    case 10: PM_WALK(true, 0, 16, false); break;
+    default: PM_WALK(true, 0, 8, false); break;
   }
 #undef PM_WALK
   return hipGetLastError();

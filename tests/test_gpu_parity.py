@@ -432,3 +432,31 @@ def test_frame_driver_matches_direct_pipeline(cornell):
         out, info = pmdist.frame(be, 0, 1, None, rgba)
         assert info["n_global"] == gmap.n and info["n_caustic"] == cmap.n
         assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("mode", ["0", "4", "5", "10", "11"])
+def test_gather_modes_bitwise(cornell, monkeypatch, mode):
+    """Every PM_GATHER_MODE walk returns the default gather's bits (pm_gather
+    and a render), incl. on an empty map."""
+    import pm_amd
+    meshes, lights = cornell
+    gs = pm_amd.Scene(meshes)
+    g = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, False)
+    c = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, True)
+    gm, cm = pm_amd.load_photons(g, c)
+    rng = np.random.default_rng(7)
+    gn = g.cpu().numpy()
+    q = gn[rng.integers(0, len(gn), 4000), 0:3] + rng.normal(scale=2.0, size=(4000, 3)).astype(np.float32)
+    q = torch.from_numpy(q.astype(np.float32)).cuda()
+    brdf = torch.from_numpy(rng.uniform(0, 0.4, size=4000).astype(np.float32)).cuda()
+    empty = torch.zeros((0, 10), dtype=torch.float32, device="cuda")
+    em, _ = pm_amd.load_photons(empty, empty)
+    W, H = 40, 30
+    cam = pm_amd.setup_camera((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
+    ref = [pm_amd.gather_photons(m, q, brdf).cpu().numpy() for m in (gm, cm, em)]
+    rref = pm_amd.render(gs, cam, W, H, 1, 30, (1, 1, 1), lights, gm, cm)[1].cpu().numpy()
+    monkeypatch.setenv("PM_GATHER_MODE", mode)
+    for m, r in zip((gm, cm, em), ref):
+        assert np.array_equal(_bits(pm_amd.gather_photons(m, q, brdf).cpu().numpy()), _bits(r))
+    got = pm_amd.render(gs, cam, W, H, 1, 30, (1, 1, 1), lights, gm, cm)[1].cpu().numpy()
+    assert np.array_equal(_bits(got), _bits(rref))
