@@ -439,12 +439,32 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, const uint32_t* v
         const float4 c4 = cres[cidx[v]];
         const v3 caustics = {c4.x, c4.y, c4.z};
         v3 diffuse = {0.f, 0.f, 0.f};
-        for (int j = 0; j < kNumDiffuseSamples; j++) {
-          const int64_t gi = v * kNumDiffuseSamples + j;
-          if (!O.gvalid[gi]) continue;
-          const float4 g4 = gres[gidx[gi]];
-          const float4 al = O.galb[gi];
-          diffuse = add(diffuse, mulv(v3{g4.x, g4.y, g4.z}, v3{al.x, al.y, al.z}));
+        // this vertex's 20 sample flags as five 16-B loads (rows are 80 B, 16-B
+        // aligned): per-lane scalar loads 80 B apart thrashed L1/L2 (~16 GB of
+        // fetches per launch). Valid samples are consecutive in gres.
+        static_assert(kNumDiffuseSamples % 4 == 0, "vector rows");
+        uint32_t gv[kNumDiffuseSamples];
+        const uint4* gv4 = reinterpret_cast<const uint4*>(O.gvalid + v * kNumDiffuseSamples);
+#pragma unroll
+        for (int k = 0; k < kNumDiffuseSamples / 4; k++) {
+          const uint4 t = gv4[k];
+          gv[4 * k] = t.x; gv[4 * k + 1] = t.y; gv[4 * k + 2] = t.z; gv[4 * k + 3] = t.w;
+        }
+        bool anyv = false;
+#pragma unroll
+        for (int j = 0; j < kNumDiffuseSamples; j++) anyv |= gv[j] != 0u;
+        if (anyv) {
+          uint32_t r = 0xFFFFFFFFu;
+#pragma unroll
+          for (int j = 0; j < kNumDiffuseSamples; j++)
+            if (gv[j] && r == 0xFFFFFFFFu) r = gidx[v * kNumDiffuseSamples + j];
+#pragma unroll
+          for (int j = 0; j < kNumDiffuseSamples; j++) {
+            if (!gv[j]) continue;
+            const float4 g4 = gres[r++];
+            const float4 al = O.galb[v * kNumDiffuseSamples + j];
+            diffuse = add(diffuse, mulv(v3{g4.x, g4.y, g4.z}, v3{al.x, al.y, al.z}));
+          }
         }
         diffuse = divf(diffuse, (float)kNumDiffuseSamples);
         const float4 ab = O.valb[v];
