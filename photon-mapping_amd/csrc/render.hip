@@ -3,24 +3,24 @@
 // Restates simpleRayGen / tracePath / ray_colour (ray-tracer/cuda/deviceCode.cu:
 // 25-231) and reflect_or_refract_ray / calculate_refracted / specularBrdf
 // (ray-tracer/cuda/shading.h:20-91) as a wavefront pipeline:
-//   1. k_count_paths  per pixel: camera path only (no shadow / diffuse rays)
-//                     -> number of ray_colour calls (path vertices). RNG use of
-//                     the 20 diffuse samples is replayed (it is independent of
-//                     what the diffuse rays hit), so the path is exact.
-//   2. scan           -> deterministic vertex slots per pixel.
-//   3. k_paths        per pixel: the camera path again; writes per-vertex
-//                     records, the caustic query, and EMITS the shadow rays and
-//                     the 20 final-gather rays per vertex into fixed slots;
+//   1. k_paths        per pixel: the camera path; writes per-vertex records
+//                     and the caustic query, and EMITS the shadow rays and the
+//                     20 final-gather rays per vertex into fixed slots. The
+//                     first vertex of each sample has a fixed slot; later ones
+//                     take continuation slots (wave-aggregated atomic) linked
+//                     by `next`, so no counting pass replays the paths;
 //      k_diffuse_rays / k_shadow_rays trace them (lean traversal kernels at
 //                     high occupancy), k_direct sums the direct light in the
 //                     reference's order.
-//   4. compaction of valid queries, k_gather (knn.hip) per query.
-//   5. k_resolve      per pixel: replays ray_colour's colour arithmetic in the
-//                     reference's order with the gathered radiance.
+//   2. compaction of valid queries, k_gather (knn.hip) per query.
+//   3. k_resolve      per pixel: replays ray_colour's colour arithmetic in the
+//                     reference's order with the gathered radiance, following
+//                     each sample's vertex links.
 // Gathers never steer control flow, so this is bitwise the megakernel result.
 // Reference UB is defined as in SURVEY §5.1-18: per-pixel hit record and the
 // diffuse rays' hit records are zero-initialised; a miss keeps the stale record.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -136,40 +136,6 @@ __device__ __forceinline__ v3 camera_dir(const RenderArgs& A, int px, int py, ui
   return normalize(add(add(A.d00, smul(su, A.du)), smul(sv, A.dv)));
 }
 
-__global__ __launch_bounds__(kRBlock) void k_count_paths(DevScene S, RenderArgs A, uint32_t* cnt, int* overflow) {
-  __shared__ int stack[kStackDepth * kRBlock];
-  const int64_t tid = (int64_t)blockIdx.x * kRBlock + threadIdx.x;
-  int px, py;
-  if (!pixel_of(A, tid, px, py)) {
-    if ((tid >> 8) < A.my_tiles) cnt[tid] = 0;
-    return;
-  }
-  int* st = stack + threadIdx.x;
-  uint32_t rng = lcg_init((uint32_t)px, (uint32_t)py);
-  HitRec hr;
-  hr.hitpoint = hr.normal = {0.f, 0.f, 0.f};
-  hr.m0 = hr.m1 = make_float4(0.f, 0.f, 0.f, 0.f);
-  uint32_t V = 0;
-  for (int s = 0; s < A.spp; s++) {
-    v3 ro = A.cam_pos;
-    v3 rd = camera_dir(A, px, py, rng);
-    for (int d = 0; d < A.depth; d++) {
-      V++;
-      if (trace_closest(S, ro, rd, kEPS, kINFTY, hr, st, overflow)) {
-        const float diffuse_brdf = hr.m0.w / kPI;
-        for (int k = 0; k < kNumDiffuseSamples && diffuse_brdf > 0.f; k++) (void)diffuse_direction(hr.normal, rng);
-      }
-      bool absorbed;
-      float coef;
-      const v3 od = reflect_or_refract(hr, rd, hr.normal, rng, absorbed, coef);
-      if (absorbed) break;
-      ro = hr.hitpoint;
-      rd = od;
-    }
-  }
-  cnt[tid] = V;
-}
-
 struct PathOut {
   float4* vdirect;    // direct term (or sky colour for a miss)
   float4* vatt;       // attenuation at this vertex
@@ -185,27 +151,49 @@ struct PathOut {
   float4* sterm;      // [nl * v + l] (ldn, inv, bs, 0) of the direct-light term
   uint32_t* svis;     // [nl * v + l] 1 = light visible
   unsigned long long* rays;
+  int32_t* next;      // next vertex of the same sample, -1 after the last
+  uint32_t* ovf;      // continuation-slot counter (slots nbase + k)
+  int64_t nbase;      // first vertex of (thread t, sample s) is slot t * spp + s
+  int64_t cap;        // continuation slots available
 };
 
-__global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths(DevScene S, RenderArgs A, const uint32_t* voff, PathOut O,
+// Vertex slots without a counting pass: the first vertex of (thread t, sample
+// s) is slot t * spp + s; a path that continues takes its next slot from the
+// continuation area (one atomic per wave and depth step) and links it with
+// O.next. Every per-vertex kernel is order-agnostic and k_resolve follows the
+// links, so results do not depend on the slot order. (The counting pass replayed
+// every camera path once more: ~3.3 ms, mostly the latency chain of the few
+// long specular paths.) Threads outside the image mark their base slots empty.
+__global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths(DevScene S, RenderArgs A, PathOut O,
                                                    int* overflow) {
   __shared__ int stack[kStackDepth * kRBlock];
   const int64_t tid = (int64_t)blockIdx.x * kRBlock + threadIdx.x;
   int px, py;
   const bool valid = pixel_of(A, tid, px, py);
   uint32_t nrays = 0;
+  if (!valid && (tid >> 8) < A.my_tiles) {
+    for (int s = 0; s < A.spp; s++) {
+      const int64_t v = tid * A.spp + s;
+      O.vflags[v] = VF_MISS | VF_LAST;
+      O.cvalid[v] = 0;
+      O.next[v] = -1;
+#pragma unroll 1
+      for (int j = 0; j < kNumDiffuseSamples; j++) O.gvalid[v * kNumDiffuseSamples + j] = 0;
+      for (int l = 0; l < A.nl; l++) O.sray[v * A.nl + l] = make_float4(0.f, 0.f, 0.f, -1.f);
+    }
+  }
   if (valid) {
     int* st = stack + threadIdx.x;
     uint32_t rng = lcg_init((uint32_t)px, (uint32_t)py);
     HitRec hr;
     hr.hitpoint = hr.normal = {0.f, 0.f, 0.f};
     hr.m0 = hr.m1 = make_float4(0.f, 0.f, 0.f, 0.f);
-    int64_t v = voff[tid];
     for (int s = 0; s < A.spp; s++) {
+      int64_t v = tid * A.spp + s;
       v3 ro = A.cam_pos;
       v3 rd = camera_dir(A, px, py, rng);
       v3 att = {1.f, 1.f, 1.f};
-      for (int d = 0; d < A.depth; d++, v++) {
+      for (int d = 0; d < A.depth; d++) {
         nrays++;
         const bool hit = trace_closest(S, ro, rd, kEPS, kINFTY, hr, st, overflow);
         O.vatt[v] = make_float4(att.x, att.y, att.z, 0.f);
@@ -266,10 +254,21 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths
         const bool last = absorbed || d == A.depth - 1;
         if (last) fl |= VF_LAST;
         O.vflags[v] = fl;
-        if (absorbed) {
-          v++;
-          break;
+        // continuation slot (wave-aggregated atomic)
+        const uint64_t m = __ballot(!last);
+        int64_t nv = -1;
+        if (m) {
+          const int lane = threadIdx.x & 63;
+          const int leader = __ffsll((long long)m) - 1;
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(O.ovf, (uint32_t)__popcll(m));
+          base = (uint32_t)__shfl((int)base, leader);
+          const uint32_t k = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+          if (!last) nv = (int64_t)k < O.cap ? O.nbase + (int64_t)k : -1;   // full: the host reruns
         }
+        O.next[v] = (int32_t)nv;
+        if (last || nv < 0) break;
+        v = nv;
         att = mulv(att, smul(coef, v3{hr.m0.x, hr.m0.y, hr.m0.z}));
         ro = hr.hitpoint;
         rd = od;
@@ -415,19 +414,16 @@ static hipError_t gather_sorted(const pm_photon_map* m, SortedQueries& Q, float4
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_resolve(RenderArgs A, const uint32_t* voff, const uint32_t* cnt,
-                                                 PathOut O, const uint32_t* cidx, const float4* cres,
+__global__ __launch_bounds__(256) void k_resolve(RenderArgs A, PathOut O, const uint32_t* cidx, const float4* cres,
                                                  const uint32_t* gidx, const float4* gres, uint32_t* rgba,
                                                  float* rgb) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int px, py;
   if (!pixel_of(A, tid, px, py)) return;
-  int64_t v = voff[tid];
-  const int64_t vend = v + cnt[tid];
   v3 fc = {0.f, 0.f, 0.f};
-  for (int s = 0; s < A.spp && v < vend; s++) {
+  for (int s = 0; s < A.spp && A.depth > 0; s++) {
     v3 colour = {0.f, 0.f, 0.f};
-    for (; v < vend;) {
+    for (int64_t v = tid * A.spp + s; v >= 0;) {
       const uint32_t fl = O.vflags[v];
       const float4 a4 = O.vatt[v];
       const v3 att = {a4.x, a4.y, a4.z};
@@ -475,8 +471,8 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, const uint32_t* v
              kDiffuseFactor * diffuse.z + kCausticsFactor * caustics.z + kDirectLightFactor * d4.z};
       }
       colour = add(colour, mulv(c, att));
-      v++;
       if (fl & VF_LAST) break;
+      v = O.next[v];
     }
     fc = add(fc, colour);
   }
@@ -502,8 +498,9 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, const uint32_t* v
 struct pm_render_job {
   pmd::RenderArgs A;
   pmd::DevBuf<pmd::LightR> dl;
-  int64_t nthreads = 0, NV = 0, NG = 0, NS = 0;
-  pmd::DevBuf<uint32_t> cnt, voff, tot;
+  int64_t nthreads = 0, NV = 0, NG = 0, NS = 0, nbase = 0, cap = 0;
+  pmd::DevBuf<uint32_t> ovf;
+  pmd::DevBuf<int32_t> next;
   pmd::DevBuf<float4> vdirect, vatt, valb, cq, gq, galb, gdir, sray, sterm, cdense, gdense, cres, gres;
   pmd::DevBuf<uint32_t> vflags, cvalid, gvalid, cidx, gidx, ctot, gtot, svis;
   pmd::DevBuf<unsigned long long> rays;
@@ -558,46 +555,61 @@ hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light*
   J->nthreads = nthreads;
   if (nthreads == 0) return hipStreamSynchronize(s);
   const DevScene S = sc->view();
-  J->cnt.alloc(nthreads);
-  J->voff.alloc(nthreads);
-  J->tot.alloc(1);
-  if (!J->cnt.p || !J->voff.p || !J->tot.p) return hipErrorOutOfMemory;
-  uint32_t V = 0;
-  {
+  const int64_t nbase = A.depth > 0 ? nthreads * A.spp : 0;
+  J->nbase = nbase;
+  J->ovf.alloc(1);
+  J->rays.alloc(1);
+  J->ctot.alloc(1);
+  J->gtot.alloc(1);
+  if (!J->ovf.p || !J->rays.p || !J->ctot.p || !J->gtot.p) return hipErrorOutOfMemory;
+  // continuation slots: a guess first (one per sample, or the last frame's
+  // need); if it was short, k_paths reruns with a larger area
+  static thread_local int64_t last_need = 0;
+  int64_t cap = std::max<int64_t>(std::max<int64_t>(nbase, last_need + last_need / 8), 4096);
+  if (const char* ce = std::getenv("PM_RENDER_CAP")) cap = std::max<int64_t>(1, std::atoll(ce));   // tests: force a rerun
+  uint32_t used = 0;
+  for (int attempt = 0;; attempt++) {
+    const int64_t NV = nbase + cap, NG = NV * kNumDiffuseSamples, NS = NV * nl;
+    for (auto* b : {&J->vdirect, &J->vatt, &J->valb, &J->cq}) b->alloc(NV);
+    for (auto* b : {&J->gq, &J->galb, &J->gdir}) b->alloc(NG);
+    for (auto* b : {&J->vflags, &J->cvalid, &J->cidx}) b->alloc(NV);
+    for (auto* b : {&J->gvalid, &J->gidx}) b->alloc(NG);
+    J->next.alloc(NV);
+    J->sray.alloc(NS);
+    J->sterm.alloc(NS);
+    J->svis.alloc(NS);
+    if (NV > 0 && (!J->vdirect.p || !J->vatt.p || !J->valb.p || !J->cq.p || !J->gq.p || !J->galb.p ||
+                   !J->vflags.p || !J->cvalid.p || !J->gvalid.p || !J->cidx.p || !J->gidx.p || !J->gdir.p ||
+                   !J->next.p))
+      return hipErrorOutOfMemory;
+    if (NS > 0 && (!J->sray.p || !J->sterm.p || !J->svis.p)) return hipErrorOutOfMemory;
+    if (nbase == 0) break;
+    PathOut O{J->vdirect.p, J->vatt.p, J->valb.p, J->vflags.p, J->cq.p, J->cvalid.p, J->gq.p, J->galb.p,
+              J->gvalid.p,  J->gdir.p, J->sray.p, J->sterm.p, J->svis.p, J->rays.p,  J->next.p, J->ovf.p,
+              nbase,        cap};
     PhaseTimer tm(PH_PATHS, s);
-    k_count_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, J->cnt.p, sc->overflow.p);
+    PM_HIP_TRY(hipMemsetAsync(J->rays.p, 0, 8, s));
+    PM_HIP_TRY(hipMemsetAsync(J->ovf.p, 0, 4, s));
+    k_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, O, sc->overflow.p);
     PM_HIP_TRY(hipGetLastError());
-    PM_HIP_TRY(exclusive_scan_u32(J->cnt.p, J->voff.p, nthreads, J->tot.p, s));
-    PM_HIP_TRY(hipMemcpyAsync(&V, J->tot.p, 4, hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipMemcpyAsync(&used, J->ovf.p, 4, hipMemcpyDeviceToHost, s));
     PM_HIP_TRY(hipStreamSynchronize(s));
+    if ((int64_t)used <= cap) break;
+    // paths cut short by a full area stopped requesting slots, so `used` is a
+    // lower bound: grow geometrically, then fall back to the worst case
+    const int64_t worst = nbase * std::max(A.depth - 1, 1);
+    if (cap >= worst) return hipErrorUnknown;   // cannot happen: every path fits
+    cap = attempt < 3 ? std::min(worst, std::max<int64_t>(2 * (int64_t)used, 4 * cap)) : worst;
   }
-  const int64_t NV = V, NG = (int64_t)V * kNumDiffuseSamples, NS = NV * nl;
+  last_need = used;
+  J->cap = cap;
+  const int64_t NV = nbase + (int64_t)used, NG = NV * kNumDiffuseSamples, NS = NV * nl;
   J->NV = NV;
   J->NG = NG;
   J->NS = NS;
-  for (auto* b : {&J->vdirect, &J->vatt, &J->valb, &J->cq}) b->alloc(NV);
-  for (auto* b : {&J->gq, &J->galb, &J->gdir}) b->alloc(NG);
-  for (auto* b : {&J->vflags, &J->cvalid, &J->cidx}) b->alloc(NV);
-  for (auto* b : {&J->gvalid, &J->gidx}) b->alloc(NG);
-  J->sray.alloc(NS);
-  J->sterm.alloc(NS);
-  J->svis.alloc(NS);
-  J->ctot.alloc(1);
-  J->gtot.alloc(1);
-  J->rays.alloc(1);
-  if (NV > 0 && (!J->vdirect.p || !J->vatt.p || !J->valb.p || !J->cq.p || !J->gq.p || !J->galb.p ||
-                 !J->vflags.p || !J->cvalid.p || !J->gvalid.p || !J->cidx.p || !J->gidx.p || !J->gdir.p))
-    return hipErrorOutOfMemory;
-  if (NS > 0 && (!J->sray.p || !J->sterm.p || !J->svis.p)) return hipErrorOutOfMemory;
-  if (!J->ctot.p || !J->gtot.p || !J->rays.p) return hipErrorOutOfMemory;
-  PathOut O{J->vdirect.p, J->vatt.p, J->valb.p, J->vflags.p, J->cq.p,   J->cvalid.p, J->gq.p,
-            J->galb.p,    J->gvalid.p, J->gdir.p, J->sray.p,  J->sterm.p, J->svis.p,   J->rays.p};
   uint32_t NC = 0, NGv = 0;
   {
     PhaseTimer tm(PH_PATHS, s);
-    PM_HIP_TRY(hipMemsetAsync(J->rays.p, 0, 8, s));
-    k_paths<<<grid_for(nthreads, kRBlock), kRBlock, 0, s>>>(S, A, J->voff.p, O, sc->overflow.p);
-    PM_HIP_TRY(hipGetLastError());
     if (NG > 0) {
       k_diffuse_rays<<<grid_for(NG, kRBlock), kRBlock, 0, s>>>(S, J->cq.p, J->gdir.p, NG, J->gvalid.p, J->gq.p,
                                                                J->galb.p, sc->overflow.p);
@@ -645,7 +657,7 @@ hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light*
     px += (int64_t)std::min(16, A.W - tx * 16) * std::min(16, A.H - ty * 16);
   }
   J->stats.pixels = px;
-  J->stats.path_vertices = NV;
+  J->stats.path_vertices = (A.depth > 0 ? px * A.spp : 0) + (int64_t)used;
   J->stats.caustic_queries = NC;
   J->stats.global_queries = NGv;
   J->stats.rays = (int64_t)nr;
@@ -660,12 +672,13 @@ hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_p
     PM_HIP_TRY(gather_sorted(cmap, J->cs, J->cres.p, 0, s));
     PM_HIP_TRY(gather_sorted(gmap, J->gs, J->gres.p, 1, s));
   }
-  PathOut O{J->vdirect.p, J->vatt.p, J->valb.p, J->vflags.p, J->cq.p,   J->cvalid.p, J->gq.p,
-            J->galb.p,    J->gvalid.p, J->gdir.p, J->sray.p,  J->sterm.p, J->svis.p,   J->rays.p};
+  PathOut O{J->vdirect.p, J->vatt.p, J->valb.p, J->vflags.p, J->cq.p, J->cvalid.p, J->gq.p, J->galb.p,
+            J->gvalid.p,  J->gdir.p, J->sray.p, J->sterm.p, J->svis.p, J->rays.p,  J->next.p, J->ovf.p,
+            J->nbase,     J->cap};
   {
     PhaseTimer tm(PH_RESOLVE, s);
-    k_resolve<<<grid_for(J->nthreads, 256), 256, 0, s>>>(J->A, J->voff.p, J->cnt.p, O, J->cidx.p, J->cres.p,
-                                                         J->gidx.p, J->gres.p, rgba, rgb);
+    k_resolve<<<grid_for(J->nthreads, 256), 256, 0, s>>>(J->A, O, J->cidx.p, J->cres.p, J->gidx.p, J->gres.p, rgba,
+                                                         rgb);
     PM_HIP_TRY(hipGetLastError());
   }
   return hipStreamSynchronize(s);

@@ -460,3 +460,24 @@ def test_gather_modes_bitwise(cornell, monkeypatch, mode):
         assert np.array_equal(_bits(pm_amd.gather_photons(m, q, brdf).cpu().numpy()), _bits(r))
     got = pm_amd.render(gs, cam, W, H, 1, 30, (1, 1, 1), lights, gm, cm)[1].cpu().numpy()
     assert np.array_equal(_bits(got), _bits(rref))
+
+
+def test_render_continuation_rerun(sphere, monkeypatch):
+    """Continuation vertex slots: a 1-slot first guess overflows and the host
+    reruns k_paths with the exact count; the image and stats are unchanged."""
+    import pm_amd
+    meshes, lights = sphere
+    gs = pm_amd.Scene(meshes)
+    g = pm_amd.run_point_light_ray_gen(gs, lights, 20000, 10, False)
+    c = pm_amd.run_point_light_ray_gen(gs, lights, 20000, 10, True)
+    gmap, cmap = pm_amd.load_photons(g, c)
+    W, H = 48, 40
+    cam = pm_amd.setup_camera((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
+    a, ra = pm_amd.render(gs, cam, W, H, 2, 30, (1, 1, 1), lights, gmap, cmap)
+    sa = bytes(pm_amd.render_stats())
+    monkeypatch.setenv("PM_RENDER_CAP", "1")
+    b, rb = pm_amd.render(gs, cam, W, H, 2, 30, (1, 1, 1), lights, gmap, cmap)
+    assert bytes(pm_amd.render_stats()) == sa
+    assert pm_amd.render_stats().path_vertices > W * H * 2   # continuation vertices existed
+    assert torch.equal(a, b)
+    assert np.array_equal(_bits(ra.cpu().numpy()), _bits(rb.cpu().numpy()))
