@@ -114,8 +114,21 @@ __device__ __forceinline__ int kd_class(const float4 e, int dim, float nc, int n
 // release fences per tile, i.e. L2 write-backs across the 8 XCDs: measured
 // 7 ms per level). Traffic per element and level: 2 x (3 x 16 B + 4 B) read,
 // 3 x 16 B + 4 B written.
+// Occupancy targets (waves per SIMD, 0 = compiler's choice), build-time A/B knobs.
+#ifndef PM_KD_PART_WAVES
+#define PM_KD_PART_WAVES 0
+#endif
+#ifndef PM_KD_COUNT_WAVES
+#define PM_KD_COUNT_WAVES 0
+#endif
 constexpr int kPartThreads = 256;
-constexpr int kPartIPT = 4;
+// positions per thread (tile = 256 * IPT). Config 3 kd build: IPT 4 44.5 ms
+// (count 114 / part 142 VGPRs), IPT 2 36.4 ms (58 / 92), IPT 1 36.6 ms; forcing
+// occupancy at IPT 4 spills (49-62 ms)
+#ifndef PM_KD_IPT
+#define PM_KD_IPT 2
+#endif
+constexpr int kPartIPT = PM_KD_IPT;
 constexpr int kPartTile = kPartThreads * kPartIPT;   // positions per tile
 
 struct SegVal {   // segmented-scan value: packed (L | R << 32) count per list
@@ -215,7 +228,7 @@ __device__ __forceinline__ SegVal part_load(const float4* __restrict__ l0, const
   return th;
 }
 
-__global__ __launch_bounds__(kPartThreads) void k_kd_count(const float4* __restrict__ l0,
+__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void k_kd_count(const float4* __restrict__ l0,
                                                            const float4* __restrict__ l1,
                                                            const float4* __restrict__ l2,
                                                            const int32_t* __restrict__ tag, int64_t n, SegTab T,
@@ -242,7 +255,7 @@ __global__ __launch_bounds__(kPartThreads) void k_kd_count(const float4* __restr
 // Exclusive segmented prefix over the tile aggregates in two coalesced steps:
 // k_kd_chunkscan scans chunks of 1024 tiles (one block each) and records each
 // chunk's total; k_kd_chunkcarry scans the chunk totals in place (one block,
-// <= 1024 chunks, i.e. < 2^30 positions). k_kd_part combines the two carries.
+// 1024 chunks per round). k_kd_part combines the two carries.
 // (A single block walking all tiles cost ~115 us per level.)
 constexpr int kChunk = 1024;
 __global__ __launch_bounds__(kChunk) void k_kd_chunkscan(const SegVal* __restrict__ agg, int64_t ntiles,
@@ -258,13 +271,18 @@ __global__ __launch_bounds__(kChunk) void k_kd_chunkscan(const SegVal* __restric
 
 __global__ __launch_bounds__(kChunk) void k_kd_chunkcarry(SegVal* __restrict__ chunk_agg, int nchunks) {
   __shared__ SegVal sh[kChunk / 64];
-  const SegVal v = (int)threadIdx.x < nchunks ? chunk_agg[threadIdx.x] : seg_zero();
-  SegVal total;
-  const SegVal ex = block_seg_scan<kChunk / 64>(v, sh, total);   // every read precedes its barriers
-  if ((int)threadIdx.x < nchunks) chunk_agg[threadIdx.x] = ex;
+  SegVal run = seg_zero();
+  for (int base = 0; base < nchunks; base += kChunk) {   // one pass up to 2^20 tiles
+    const int c = base + (int)threadIdx.x;
+    const SegVal v = c < nchunks ? chunk_agg[c] : seg_zero();
+    SegVal total;
+    const SegVal ex = block_seg_scan<kChunk / 64>(v, sh, total);   // every read precedes its barriers
+    if (c < nchunks) chunk_agg[c] = seg_combine(run, ex);
+    run = seg_combine(run, total);
+  }
 }
 
-__global__ __launch_bounds__(kPartThreads) void k_kd_part(const float4* __restrict__ l0, const float4* __restrict__ l1,
+__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void k_kd_part(const float4* __restrict__ l0, const float4* __restrict__ l1,
                                                           const float4* __restrict__ l2, float4* __restrict__ o0,
                                                           float4* __restrict__ o1, float4* __restrict__ o2,
                                                           int32_t* __restrict__ tag, int64_t n, SegTab T,
@@ -317,8 +335,13 @@ __global__ __launch_bounds__(kPartThreads) void k_kd_part(const float4* __restri
 // barrier). Same rules as the global levels, so the tree is identical; the
 // bottom ~10 levels no longer cost a global read + write each.
 constexpr int kLocal = 1024;
+// From local level 4 on every sub-segment has <= 63 elements and there are 16 of
+// them: sub-segment j is finished by wave j with shuffles, a packed wave scan
+// and ds_permute (no block barriers, no LDS); same rules, same tree.
+constexpr int kLocalWaveLevel = 4;
+static_assert(kLocal / 64 == (1 << kLocalWaveLevel), "one wave per level-4 sub-segment");
 
-__global__ __launch_bounds__(kLocal) void k_kd_local(const float4* __restrict__ l0, const float4* __restrict__ l1,
+__global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_kd_local(const float4* __restrict__ l0, const float4* __restrict__ l1,
                                                      const float4* __restrict__ l2, int L0, SegTab T,
                                                      float4* __restrict__ nodes) {
   __shared__ float4 buf[3][kLocal];
@@ -329,6 +352,7 @@ __global__ __launch_bounds__(kLocal) void k_kd_local(const float4* __restrict__ 
   __shared__ float sco[kLocal / 2];
   __shared__ int32_t sid[kLocal / 2];
   __shared__ SegVal sh[kLocal / 64];
+  __shared__ float4 stage[kLocal];   // this subtree's nodes by local heap index (w = -1: none)
   const int tid = threadIdx.x;
   const int64_t t = ((int64_t)1 << L0) - 1 + blockIdx.x;
   const int B = T.b[t], S = T.s[t];
@@ -339,12 +363,14 @@ __global__ __launch_bounds__(kLocal) void k_kd_local(const float4* __restrict__ 
     for (int d = 0; d < 3; d++) buf[d][tid] = L[d][B + tid];
   }
   tag[tid] = tid < S ? 0 : -1;
+  stage[tid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
   if (tid == 0) {
     sb[0][0] = 0;
     ss[0][0] = (int16_t)S;
   }
   const int H = 32 - __clz(S);   // levels of this subtree
-  for (int k = 0; k < H; k++) {
+  const int KB = min(H, kLocalWaveLevel);   // block-wide levels; the rest run per wave
+  for (int k = 0; k < KB; k++) {
     const int cur = k & 1;
     const int nsub = 1 << k;
     __syncthreads();
@@ -365,7 +391,7 @@ __global__ __launch_bounds__(kLocal) void k_kd_local(const float4* __restrict__ 
         sdim[tid] = (uint8_t)dim;
         sco[tid] = coord_of(e, dim);
         sid[tid] = id;
-        nodes[(t + 1) * ((int64_t)1 << k) - 1 + tid] = make_float4(e.x, e.y, e.z, __int_as_float((id << 2) | dim));
+        stage[(1 << k) - 1 + tid] = make_float4(e.x, e.y, e.z, __int_as_float((id << 2) | dim));
       }
       sls[tid] = (int16_t)ls;
       if (k + 1 < H) {
@@ -408,6 +434,93 @@ __global__ __launch_bounds__(kLocal) void k_kd_local(const float4* __restrict__ 
       if (tid < S) buf[d][dst] = e[d];
     }
     if (j >= 0) tag[tid] = (int16_t)(tid < b + ls ? 2 * j : (tid == b + ls ? -1 : 2 * j + 1));
+  }
+  __syncthreads();
+  if (KB < H) {
+  // ---- wave phase: sub-segment j of local level KB (<= 63 elements) -> wave j
+  const int lane = tid & 63, j = tid >> 6;
+  const int cur = KB & 1;
+  const int b0 = sb[cur][j], sz0 = ss[cur][j];
+  const bool active = lane < sz0;
+  float4 e[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) e[d] = active ? buf[d][b0 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int p = b0 + lane;                       // this lane's position (fixed)
+  int b = b0, sz = sz0;                          // this lane's segment
+  int lnode = (1 << KB) - 1 + j;                // local heap index of this lane's segment
+  bool placed = !active;
+  for (int k = KB; k < H && sz0 > 0; k++) {
+    const int ls = placed ? 0 : left_size(sz);
+    // segment extents and median from the lanes holding them (all lanes shuffle)
+    const int lf = placed ? lane : b - b0, ll = placed ? lane : b + sz - 1 - b0;
+    float ext[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const float c = coord_of(e[d], d);
+      ext[d] = __shfl(c, ll) - __shfl(c, lf);
+    }
+    int dim = 0;
+    if (ext[1] > ext[dim]) dim = 1;
+    if (ext[2] > ext[dim]) dim = 2;
+    const float4 sel = dim == 0 ? e[0] : (dim == 1 ? e[1] : e[2]);
+    const int lm = placed ? lane : b + ls - b0;
+    const float4 m = make_float4(__shfl(sel.x, lm), __shfl(sel.y, lm), __shfl(sel.z, lm), __shfl(sel.w, lm));
+    const int nid = __float_as_int(m.w);
+    const float nc = coord_of(m, dim);
+    if (!placed && p == b + ls) stage[lnode] = make_float4(m.x, m.y, m.z, __int_as_float((nid << 2) | dim));
+    if (k + 1 == H) break;
+    // class per list, packed (L, R) counts: list d at bits 14d (L) and 14d + 7 (R)
+    uint8_t c[3];
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      c[d] = placed ? 3 : (uint8_t)kd_class(e[d], dim, nc, nid);
+      cnt |= (uint64_t)(c[d] == 0) << (14 * d) | (uint64_t)(c[d] == 2) << (14 * d + 7);
+    }
+    uint64_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t up = __shfl_up(inc, o);
+      if (lane >= o) inc += up;
+    }
+    const int lb = b - b0 - 1;   // lane before the segment (-1: none)
+    const uint64_t before = __shfl(inc, lb < 0 ? 0 : lb);
+    const uint64_t ex = inc - cnt - (lb < 0 || placed ? 0ull : before);
+    // forward permute of the three elements to their positions in the segment
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      int dst = p;
+      if (c[d] == 0) dst = b + (int)((ex >> (14 * d)) & 127);
+      else if (c[d] == 1) dst = b + ls;
+      else if (c[d] == 2) dst = b + ls + 1 + (int)((ex >> (14 * d + 7)) & 127);
+      const int a = (dst - b0) * 4;
+      e[d].x = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].x)));
+      e[d].y = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].y)));
+      e[d].z = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].z)));
+      e[d].w = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].w)));
+    }
+    // positional segment update
+    if (!placed) {
+      if (p < b + ls) {
+        sz = ls;
+        lnode = 2 * lnode + 1;
+      } else if (p == b + ls) {
+        placed = true;
+      } else {
+        b = b + ls + 1;
+        sz = sz - ls - 1;
+        lnode = 2 * lnode + 2;
+      }
+    }
+  }
+  }
+  // ---- write-out: nodes leave LDS once, level by level (contiguous heap ranges);
+  // a global store inside the level loop made every block barrier wait for it
+  __syncthreads();
+  const float4 nd = stage[tid];
+  if (__float_as_int(nd.w) >= 0) {
+    const int k = 31 - __clz(tid + 1);
+    nodes[(t + 1) * ((int64_t)1 << k) - 1 + (tid + 1 - (1 << k))] = nd;
   }
 }
 
