@@ -185,35 +185,65 @@ constexpr int kSortBlock = 256;
 constexpr int kSortRounds = 16;   // 4096 keys per tile: ~16 per digit run on write-out
 constexpr int kSortTile = kSortBlock * kSortRounds;
 
+// Per-tile digit histogram: 16 consecutive keys per thread (four 16-B loads),
+// per-wave sub-histograms in LDS (less atomic contention), summed at the end.
 __global__ __launch_bounds__(kSortBlock) void k_sort_hist(const uint32_t* keys, int64_t n, int shift,
                                                           uint32_t* hist, int nblocks) {
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  __shared__ uint32_t h[kSortBlock / 64][256];
+  const int tid = threadIdx.x, w = tid >> 6;
 #pragma unroll
-  for (int r = 0; r < kSortRounds; r++) {
-    int64_t i = base + (int64_t)r * kSortBlock + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
+  for (int k = 0; k < kSortBlock / 64; k++) h[k][tid] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kSortTile + (int64_t)tid * kSortRounds;
+  if (base + kSortRounds <= n) {
+    const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
+#pragma unroll
+    for (int r = 0; r < kSortRounds / 4; r++) {
+      const uint4 v = k4[r];
+      atomicAdd(&h[w][(v.x >> shift) & 0xFF], 1u);
+      atomicAdd(&h[w][(v.y >> shift) & 0xFF], 1u);
+      atomicAdd(&h[w][(v.z >> shift) & 0xFF], 1u);
+      atomicAdd(&h[w][(v.w >> shift) & 0xFF], 1u);
+    }
+  } else {
+    for (int r = 0; r < kSortRounds; r++)
+      if (base + r < n) atomicAdd(&h[w][(keys[base + r] >> shift) & 0xFF], 1u);
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kSortBlock / 64; k++) c += h[k][tid];
+  hist[(int64_t)tid * nblocks + blockIdx.x] = c;
 }
 
-// Stable per-tile scatter: the tile is first ranked into LDS in digit order
-// (ballot multi-split per wave, rounds in input order), then written out so
-// that consecutive threads store consecutive positions of each digit's run
-// (coalesced), instead of every element landing in a different bucket line.
+// Stable per-tile scatter. Wave w ranks the tile's w-th run of 1024 keys (all
+// 16 loads issued up front; ballot multi-split per 64 keys, wave-private digit
+// counters in LDS, no block barriers), one barrier turns the per-wave counts
+// into offsets (wave w's keys follow wave w-1's in the input, so the order is
+// stable), then the tile is ranked into LDS in digit order and written out so
+// that consecutive threads store consecutive positions of each digit's run.
+// (Loading inside 16 barrier-separated rounds left the pass latency-bound.)
 __global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const uint32_t* __restrict__ keys,
                                                              const uint32_t* __restrict__ vals,
                                                              uint32_t* __restrict__ okeys, uint32_t* __restrict__ ovals,
                                                              int64_t n, int shift, const uint32_t* __restrict__ hist,
                                                              const uint32_t* __restrict__ hoff, int nblocks) {
   __shared__ uint32_t lkey[kSortTile], lval[kSortTile];
-  __shared__ uint32_t running[256], lstart[256], gbase[256];
+  __shared__ uint32_t lstart[256], gbase[256];
   __shared__ uint32_t wcnt[kSortBlock / 64][256];
   __shared__ uint32_t wsum[kSortBlock / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int kWaveKeys = kSortTile / (kSortBlock / 64);   // 1024
+  constexpr int kSub = kWaveKeys / 64;                      // 16 sub-rounds of 64 keys
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const int64_t wbase = base + (int64_t)w * kWaveKeys;
+  uint32_t kr[kSub], vr[kSub];
+#pragma unroll
+  for (int r = 0; r < kSub; r++) {
+    const int64_t i = wbase + r * 64 + lane;
+    kr[r] = i < n ? keys[i] : 0u;
+    vr[r] = i < n ? vals[i] : 0u;
+  }
   // local digit starts = exclusive scan of this tile's histogram
   const uint32_t c = hist[(int64_t)tid * nblocks + blockIdx.x];
   uint32_t incl = c;
@@ -223,44 +253,49 @@ __global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const uint32_t* __r
     if (lane >= o) incl += up;
   }
   if (lane == 63) wsum[w] = incl;
+#pragma unroll
+  for (int k = 0; k < kSortBlock / 64; k++) wcnt[k][tid] = 0;
   __syncthreads();
   uint32_t wpre = 0;
 #pragma unroll
   for (int k = 0; k < kSortBlock / 64; k++) wpre += k < w ? wsum[k] : 0u;
   lstart[tid] = wpre + incl - c;
-  running[tid] = wpre + incl - c;
   gbase[tid] = hoff[(int64_t)tid * nblocks + blockIdx.x];
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  for (int r = 0; r < kSortRounds; r++) {
+  uint32_t rk[kSub];
 #pragma unroll
-    for (int k = 0; k < kSortBlock / 64; k++) wcnt[k][tid] = 0;
-    __syncthreads();
-    const int64_t i = base + (int64_t)r * kSortBlock + tid;
-    const bool valid = i < n;
-    const uint32_t key = valid ? keys[i] : 0u;
-    const uint32_t val = valid ? vals[i] : 0u;
-    const uint32_t dg = (key >> shift) & 0xFF;
+  for (int r = 0; r < kSub; r++) {
+    const bool valid = wbase + r * 64 + lane < n;
+    const uint32_t dg = (kr[r] >> shift) & 0xFF;
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; b++) {
       const uint64_t bal = __ballot((dg >> b) & 1);
       peers &= ((dg >> b) & 1) ? bal : ~bal;
     }
-    const uint32_t rank = (uint32_t)__popcll(peers & lt_mask);
-    if (valid && rank == 0) wcnt[w][dg] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    if (valid) {
-      uint32_t pos = running[dg] + rank;
-      for (int k = 0; k < w; k++) pos += wcnt[k][dg];
-      lkey[pos] = key;
-      lval[pos] = val;
-    }
-    __syncthreads();
-    uint32_t add = 0;
+    const uint32_t before = wcnt[w][dg];
+    const uint32_t lr = (uint32_t)__popcll(peers & lt_mask);
+    rk[r] = before + lr;
+    if (valid && lr == 0) wcnt[w][dg] = before + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  {  // per-digit offsets of each wave's keys inside the tile
+    uint32_t run = lstart[tid];
 #pragma unroll
-    for (int k = 0; k < kSortBlock / 64; k++) add += wcnt[k][tid];
-    running[tid] += add;
+    for (int k = 0; k < kSortBlock / 64; k++) {
+      const uint32_t cnt = wcnt[k][tid];
+      wcnt[k][tid] = run;
+      run += cnt;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSub; r++) {
+    if (wbase + r * 64 + lane < n) {
+      const uint32_t pos = wcnt[w][(kr[r] >> shift) & 0xFF] + rk[r];
+      lkey[pos] = kr[r];
+      lval[pos] = vr[r];
+    }
   }
   __syncthreads();
   const int tile_n = (int)min((int64_t)kSortTile, n - base);

@@ -284,7 +284,10 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths
 // Final-gather rays: closest hit from the vertex; a hit with a diffuse
 // material yields a global-map query (hitpoint, brdf) and its albedo
 // (closestHit + deviceCode.cu:120-129).
-__global__ __launch_bounds__(kRBlock) void k_diffuse_rays(DevScene S, const float4* __restrict__ cq,
+#ifndef PM_RAYS_WAVES
+#define PM_RAYS_WAVES 0   // occupancy target of k_diffuse_rays / k_shadow_rays (0: compiler's choice)
+#endif
+__global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_RAYS_WAVES) void k_diffuse_rays(DevScene S, const float4* __restrict__ cq,
                                                           const float4* __restrict__ gdir, int64_t ng,
                                                           uint32_t* __restrict__ gvalid, float4* __restrict__ gq,
                                                           float4* __restrict__ galb, int* overflow) {
@@ -312,7 +315,7 @@ __global__ __launch_bounds__(kRBlock) void k_diffuse_rays(DevScene S, const floa
 }
 
 // Shadow rays (TERMINATE_ON_FIRST_HIT): visible = no hit in (eps, dist (1 - eps)).
-__global__ __launch_bounds__(kRBlock) void k_shadow_rays(DevScene S, const float4* __restrict__ cq,
+__global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_RAYS_WAVES) void k_shadow_rays(DevScene S, const float4* __restrict__ cq,
                                                          const float4* __restrict__ sray, int nl, int64_t ns,
                                                          uint32_t* __restrict__ svis, int* overflow) {
   __shared__ int stack[kStackDepth * kRBlock];
