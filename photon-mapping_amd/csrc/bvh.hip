@@ -3,13 +3,15 @@
 // Replaces the OptiX GAS+IAS build of common/src/world.cpp:3-58 (loadGeometry:
 // one build input per mesh, owlGroupBuildAccel) and the RT-core traversal
 // behind every owl::traceRay / optixTrace. Pipeline: 30-bit Morton codes of
-// triangle centroids -> stable radix sort -> Karras hierarchy -> bottom-up
-// refit (agent-scope release/acquire hand-off between sibling threads) into
-// 64-B BVH2 nodes that carry both child boxes -> greedy top-down collapse into
-// 128-B BVH4 nodes (one cache line = four box tests), which the traversal uses.
+// triangle centroids -> stable radix sort -> PLOC clustering (default) or the
+// Karras hierarchy + bottom-up refit (agent-scope release/acquire hand-off
+// between sibling threads) into 64-B BVH2 nodes that carry both child boxes ->
+// greedy top-down collapse into 128-B BVH4 nodes (one cache line = four box
+// tests), which the traversal uses.
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "pm_internal.hpp"
@@ -148,6 +150,137 @@ __global__ void k_pack_children(float4* nodes, const int4* child, int nn) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nn) return;
   nodes[4 * i + 3] = *reinterpret_cast<const float4*>(&child[i]);
+}
+
+// ---------------------------------------------------------------- PLOC
+// Parallel locally-ordered clustering (Meister & Bittner 2018), the default
+// binary builder (PM_BVH=lbvh selects the Karras hierarchy + refit above): the
+// leaves in Morton order are the initial clusters; every iteration each cluster
+// finds its nearest neighbour within +-r positions (surface area of
+// the merged box; ties to the lower index), mutual pairs merge into a new node,
+// survivors are compacted in order. Node ids are handed out from n-2 down, so
+// the last merge (the root) is node 0, as collapse_bvh4 expects. Deterministic.
+// A tree closer to SAH quality only changes the traversal's speed: hits are
+// argmin (t, triangle id) whatever the tree.
+constexpr int kPlocRadius = 32;   // LDS window; the search radius r <= kPlocRadius (PM_PLOC_RADIUS)
+constexpr int kPlocBlock = 256;
+constexpr int kPlocDefaultRadius = 16;   // config 3 frame: r 8 168.2 ms, 16 168.5, 24 173.3, 32 175.4 (LBVH 176.4)
+
+struct Clu {   // cluster: box (lo.xyz, code bits) (hi.xyz, -)
+  float4 lo, hi;
+};
+
+__device__ __forceinline__ float merged_area(const Clu& a, const Clu& b) {
+  const float dx = fmaxf(a.hi.x, b.hi.x) - fminf(a.lo.x, b.lo.x);
+  const float dy = fmaxf(a.hi.y, b.hi.y) - fminf(a.lo.y, b.lo.y);
+  const float dz = fmaxf(a.hi.z, b.hi.z) - fminf(a.lo.z, b.lo.z);
+  return dx * dy + dy * dz + dz * dx;
+}
+
+__global__ void k_ploc_leaves(const float4* tri, int n, float pad, Clu* c) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 a = tri[3 * i], b = tri[3 * i + 1], d = tri[3 * i + 2];
+  Clu u;
+  u.lo = make_float4(fminf(fminf(a.x, b.x), d.x) - pad, fminf(fminf(a.y, b.y), d.y) - pad,
+                     fminf(fminf(a.z, b.z), d.z) - pad, __int_as_float(~i));
+  u.hi = make_float4(fmaxf(fmaxf(a.x, b.x), d.x) + pad, fmaxf(fmaxf(a.y, b.y), d.y) + pad,
+                     fmaxf(fmaxf(a.z, b.z), d.z) + pad, 0.f);
+  c[i] = u;
+}
+
+__global__ __launch_bounds__(kPlocBlock) void k_ploc_nn(const Clu* __restrict__ c, int m, int r,
+                                                        int* __restrict__ nn) {
+  __shared__ Clu sc[kPlocBlock + 2 * kPlocRadius];
+  const int b0 = blockIdx.x * kPlocBlock - kPlocRadius;
+  for (int k = threadIdx.x; k < kPlocBlock + 2 * kPlocRadius; k += kPlocBlock) {
+    const int g = b0 + k;
+    if (g >= 0 && g < m) sc[k] = c[g];
+  }
+  __syncthreads();
+  const int i = blockIdx.x * kPlocBlock + threadIdx.x;
+  if (i >= m) return;
+  const Clu me = sc[threadIdx.x + kPlocRadius];
+  float best = INFINITY;
+  int bj = -1;
+  for (int d = -r; d <= r; d++) {
+    const int j = i + d;
+    if (d == 0 || j < 0 || j >= m) continue;
+    const float a = merged_area(me, sc[threadIdx.x + kPlocRadius + d]);
+    if (a < best) {   // ascending j: ties keep the lower index
+      best = a;
+      bj = j;
+    }
+  }
+  nn[i] = bj;
+}
+
+// merge_lo: i is the lower index of a mutual pair; keep: i survives the compaction
+__global__ void k_ploc_flags(const int* __restrict__ nn, int m, uint32_t* __restrict__ merge_lo,
+                             uint32_t* __restrict__ keep) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const int j = nn[i];
+  const bool mutual = j >= 0 && nn[j] == i;
+  merge_lo[i] = mutual && i < j;
+  keep[i] = !(mutual && i > j);
+}
+
+__global__ void k_ploc_merge(Clu* __restrict__ c, const int* __restrict__ nn, int m,
+                             const uint32_t* __restrict__ merge_lo, const uint32_t* __restrict__ moff, int top,
+                             float4* __restrict__ bin) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m || !merge_lo[i]) return;
+  const Clu a = c[i], b = c[nn[i]];
+  const int node = top - 1 - (int)moff[i];
+  float* f = reinterpret_cast<float*>(&bin[4 * node]);   // (l box, r box), then child codes
+  f[0] = a.lo.x; f[1] = a.hi.x; f[2] = a.lo.y; f[3] = a.hi.y; f[4] = a.lo.z; f[5] = a.hi.z;
+  f[6] = b.lo.x; f[7] = b.hi.x; f[8] = b.lo.y; f[9] = b.hi.y; f[10] = b.lo.z; f[11] = b.hi.z;
+  bin[4 * node + 3] = make_float4(a.lo.w, b.lo.w, 0.f, 0.f);
+  Clu u;
+  u.lo = make_float4(fminf(a.lo.x, b.lo.x), fminf(a.lo.y, b.lo.y), fminf(a.lo.z, b.lo.z), __int_as_float(node));
+  u.hi = make_float4(fmaxf(a.hi.x, b.hi.x), fmaxf(a.hi.y, b.hi.y), fmaxf(a.hi.z, b.hi.z), 0.f);
+  c[i] = u;
+}
+
+__global__ void k_ploc_compact(const Clu* __restrict__ c, int m, const uint32_t* __restrict__ keep,
+                               const uint32_t* __restrict__ koff, Clu* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m || !keep[i]) return;
+  out[koff[i]] = c[i];
+}
+
+static hipError_t build_ploc(const float4* tri, int n, float pad, float4* bin, hipStream_t s) {
+  DevBuf<Clu> ca(n), cb(n);
+  DevBuf<int> nn(n);
+  DevBuf<uint32_t> mlo(n), moff(n), keep(n), koff(n), tot(2);
+  if (!ca.p || !cb.p || !nn.p || !mlo.p || !moff.p || !keep.p || !koff.p || !tot.p) return hipErrorOutOfMemory;
+  k_ploc_leaves<<<grid_for(n, 256), 256, 0, s>>>(tri, n, pad, ca.p);
+  PM_HIP_TRY(hipGetLastError());
+  Clu *cur = ca.p, *nxt = cb.p;
+  const char* renv = std::getenv("PM_PLOC_RADIUS");
+  const int r = renv ? std::min(kPlocRadius, std::max(1, std::atoi(renv))) : kPlocDefaultRadius;
+  int m = n, top = n - 1;   // internal node ids top-1 .. 0
+  while (m > 1) {
+    k_ploc_nn<<<grid_for(m, kPlocBlock), kPlocBlock, 0, s>>>(cur, m, r, nn.p);
+    PM_HIP_TRY(hipGetLastError());
+    k_ploc_flags<<<grid_for(m, 256), 256, 0, s>>>(nn.p, m, mlo.p, keep.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(exclusive_scan_u32(mlo.p, moff.p, m, tot.p, s));
+    PM_HIP_TRY(exclusive_scan_u32(keep.p, koff.p, m, tot.p + 1, s));
+    k_ploc_merge<<<grid_for(m, 256), 256, 0, s>>>(cur, nn.p, m, mlo.p, moff.p, top, bin);
+    PM_HIP_TRY(hipGetLastError());
+    k_ploc_compact<<<grid_for(m, 256), 256, 0, s>>>(cur, m, keep.p, koff.p, nxt);
+    PM_HIP_TRY(hipGetLastError());
+    uint32_t h[2] = {0, 0};
+    PM_HIP_TRY(hipMemcpyAsync(h, tot.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    if (h[0] == 0) return hipErrorUnknown;   // cannot happen: the closest pair is mutual
+    top -= (int)h[0];
+    m = (int)h[1];
+    std::swap(cur, nxt);
+  }
+  return top == 0 ? hipStreamSynchronize(s) : hipErrorUnknown;
 }
 
 // ---------------------------------------------------------------- BVH4 collapse
@@ -327,6 +460,11 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s
   PM_HIP_TRY(radix_sort_pairs(codes.p, order.p, n, 30, s));
   k_gather_tris<<<grid_for(n, 256), 256, 0, s>>>(tri_orig.p, order.p, n, sc->tri.p);
   PM_HIP_TRY(hipGetLastError());
+  const char* benv = std::getenv("PM_BVH");
+  if (!(benv && std::strcmp(benv, "lbvh") == 0)) {
+    PM_HIP_TRY(build_ploc(sc->tri.p, n, pad, bin.p, s));
+    return collapse_bvh4(bin.p, nn, sc, s);
+  }
   PM_HIP_TRY(hipMemsetAsync(pint.p, 0, sizeof(int) * nn, s));
   k_hierarchy<<<grid_for(n - 1, 256), 256, 0, s>>>(codes.p, n, child.p, pint.p, pleaf.p);
   PM_HIP_TRY(hipGetLastError());
