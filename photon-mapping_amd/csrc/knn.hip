@@ -225,13 +225,13 @@ __device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, 
     const int child = 2 * curr + 1;
     const int w = __float_as_int(nd.w);
     const int dim = w & 3;
-    const float diff = (dim == 0 ? q.x : (dim == 1 ? q.y : q.z)) - (dim == 0 ? nd.x : (dim == 1 ? nd.y : nd.z));
+    const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
+    const float diff = dim == 0 ? dx : (dim == 1 ? dy : dz);   // = q[dim] - nd[dim]
     const int side = diff > 0.f ? 1 : 0;
     const int close_c = child + side, far_c = child + 1 - side;
     const int parent = ((curr + 1) >> 1) - 1;
     const bool down = prev < child;
     const bool test = (down && close_c >= n) || prev == close_c;
-    const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
     const float d2 = dx * dx + dy * dy + dz * dz;
     const double key = key_make(d2, (uint32_t)(w >> 2));
     const bool cand = walking && test && key < list[K - 1];
@@ -309,16 +309,19 @@ __device__ __forceinline__ v3 radiance(const double (&list)[kKNearest], const fl
 }
 
 // TAG only separates the global-map launch into its own kernel symbol (rocprof).
+// perm (optional): lane i takes query perm[i] and writes its result there, so a
+// caller can walk in Morton order without permuted / unpermuted copies.
 template <int TAG, bool POST, int QP, int QL = 0, bool LEAN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
-    int64_t nq, float4* __restrict__ out) {
+    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm) {
   __shared__ double lq[QL > 0 ? QL * 256 : 1];
   // plain block order on purpose: consecutive blocks (Morton-adjacent queries)
   // spread over the 8 XCDs keep ONE narrow window of the tree live in the
   // shared Infinity Cache; an XCD-contiguous remap measured 9 % slower.
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = i < nq;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = i0 < nq;
+  const int64_t i = (valid && perm) ? (int64_t)perm[i0] : i0;
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   double list[kKNearest];
   const float R2 = kKMaxDistance * kKMaxDistance;
@@ -351,11 +354,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 template <bool POST, int QP, int QL = 0>
 __global__ __launch_bounds__(256) void k_gather_stats(const float4* __restrict__ nodes, int n,
                                                       const float4* __restrict__ qb, int64_t nq,
-                                                      unsigned long long* acc) {
+                                                      unsigned long long* acc, const uint32_t* __restrict__ perm) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   KnnCounters kc;
   const bool valid = i < nq;
-  const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 qq = valid ? qb[perm ? (int64_t)perm[i] : i] : make_float4(0.f, 0.f, 0.f, 0.f);
   double list[kKNearest];
   __shared__ double lq[QL > 0 ? QL * 256 : 1];
   knn_walk<kKNearest, POST, QP, true, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, kKMaxDistance * kKMaxDistance, valid,
@@ -370,15 +373,16 @@ __global__ __launch_bounds__(256) void k_gather_stats(const float4* __restrict__
   }
 }
 
-static void gather_stats(const pm_photon_map* m, const float4* qb, int64_t nq, int mode, hipStream_t s) {
+static void gather_stats(const pm_photon_map* m, const float4* qb, int64_t nq, int mode, hipStream_t s,
+                         const uint32_t* perm) {
   DevBuf<unsigned long long> acc(8);
   if (!acc.p || hipMemsetAsync(acc.p, 0, 64, s) != hipSuccess) return;
   const int g = grid_for(nq, 256);
-  if (mode == 4) k_gather_stats<true, 0><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
-  else if (mode == 5) k_gather_stats<true, 4><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
-  else if (mode == 0) k_gather_stats<false, 0><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
-  else if (mode == 10) k_gather_stats<true, 0, 16><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
-  else k_gather_stats<true, 0, 8><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p);
+  if (mode == 4) k_gather_stats<true, 0><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p, perm);
+  else if (mode == 5) k_gather_stats<true, 4><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p, perm);
+  else if (mode == 0) k_gather_stats<false, 0><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p, perm);
+  else if (mode == 10) k_gather_stats<true, 0, 16><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p, perm);
+  else k_gather_stats<true, 0, 8><<<g, 256, 0, s>>>(m->nodes.p, (int)m->n, qb, nq, acc.p, perm);
   unsigned long long h[8] = {};
   if (hipMemcpyAsync(h, acc.p, 64, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
     return;
@@ -430,7 +434,7 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
 }
 
 hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,
-                         int tag) {
+                         int tag, const uint32_t* perm) {
   if (nq <= 0) return hipSuccess;
   // A/B knob (read per launch), all variants return identical bits:
   //  11 (default) mode 9 with the lean step (knn_walk_lean)   62.3 ms
@@ -442,12 +446,12 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   // (config 3 global map; depths 4 / 6: 67.3 / 66.4 ms)
   const char* env = std::getenv("PM_GATHER_MODE");
   const int mode = env ? std::atoi(env) : 11;
-  if (std::getenv("PM_GATHER_STATS")) gather_stats(m, qb, nq, mode, s);
+  if (std::getenv("PM_GATHER_STATS")) gather_stats(m, qb, nq, mode, s, perm);
   const int g = grid_for(nq, 256);
   const int n = (int)m->n;
 #define PM_WALK(P, Q, L, LEAN)                                                                          \
-  (tag == 1 ? (k_gather<1, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out))    \
-            : (k_gather<0, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out)))
+  (tag == 1 ? (k_gather<1, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm))  \
+            : (k_gather<0, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm)))
   switch (mode) {
     case 11: PM_WALK(true, 0, 8, true); break;
     case 0: PM_WALK(false, 0, 0, false); break;

@@ -69,6 +69,6 @@ hipError_t kd_build(const float4* d_elems, int64_t n, float4* d_nodes, hipStream
 // K = 50 gather (gatherPhotons) for a batch of queries.
 // tag 0: API / caustic-map launches, 1: global-map launch (separate kernel symbol for rocprof)
 hipError_t launch_gather(const pm_photon_map* m, const float4* d_query /*pos, brdf*/, int64_t nq,
-                         float4* d_out, hipStream_t s, int tag = 0);
+                         float4* d_out, hipStream_t s, int tag = 0, const uint32_t* perm = nullptr);
 
 }  // namespace pmd

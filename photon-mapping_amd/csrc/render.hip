@@ -369,52 +369,39 @@ __global__ void k_query_morton(const float4* q, int64_t n, float3 lo, float3 inv
   keys[i] = morton30(p.x, p.y, p.z, lo, inv);
   perm[i] = (uint32_t)i;
 }
-__global__ void k_permute_q(const float4* src, const uint32_t* perm, int64_t n, float4* dst) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  dst[i] = src[perm[i]];
-}
-__global__ void k_unpermute_q(const float4* src, const uint32_t* perm, int64_t n, float4* dst) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  dst[perm[i]] = src[i];
-}
-
 // Gathers run in Morton order of the query points (a pure permutation:
 // results are bitwise unchanged) so the lanes of a wave walk the same kd-tree
-// nodes. The sort needs only the scene bounds, so it belongs to render_begin.
+// nodes; k_gather reads and writes through the permutation. The sort needs only
+// the scene bounds, so it belongs to render_begin.
 struct SortedQueries {
-  DevBuf<uint32_t> keys, perm;
-  DevBuf<float4> qs, rs;
+  DevBuf<uint32_t> keys, perm;   // perm: Morton order of the dense queries
+  const float4* dense = nullptr;
   int64_t n = 0;
 };
 
 static hipError_t sort_queries(const float4* dense, int64_t n, const pm_box& bb, SortedQueries& Q, hipStream_t s) {
   Q.n = n;
+  Q.dense = dense;
   if (n <= 0) return hipSuccess;
   Q.keys.alloc(n);
   Q.perm.alloc(n);
-  Q.qs.alloc(n);
-  Q.rs.alloc(n);
-  if (!Q.keys.p || !Q.perm.p || !Q.qs.p || !Q.rs.p) return hipErrorOutOfMemory;
+  if (!Q.keys.p || !Q.perm.p) return hipErrorOutOfMemory;
   const float3 lo = make_float3(bb.lower.x, bb.lower.y, bb.lower.z);
   const float ex = bb.upper.x - bb.lower.x, ey = bb.upper.y - bb.lower.y, ez = bb.upper.z - bb.lower.z;
   const float3 inv = make_float3(ex > 0.f ? 1.0f / ex : 0.f, ey > 0.f ? 1.0f / ey : 0.f, ez > 0.f ? 1.0f / ez : 0.f);
   k_query_morton<<<grid_for(n, 256), 256, 0, s>>>(dense, n, lo, inv, Q.keys.p, Q.perm.p);
   PM_HIP_TRY(hipGetLastError());
-  PM_HIP_TRY(radix_sort_pairs(Q.keys.p, Q.perm.p, n, 30, s));
-  k_permute_q<<<grid_for(n, 256), 256, 0, s>>>(dense, Q.perm.p, n, Q.qs.p);
-  return hipGetLastError();
+  return radix_sort_pairs(Q.keys.p, Q.perm.p, n, 30, s);
 }
 
 static hipError_t gather_sorted(const pm_photon_map* m, SortedQueries& Q, float4* res, int tag, hipStream_t s) {
   if (Q.n <= 0) return hipSuccess;
   {
     PhaseTimer tg(tag == 1 ? PH_GATHER_GLOBAL : PH_COUNT, s);
-    PM_HIP_TRY(launch_gather(m, Q.qs.p, Q.n, Q.rs.p, s, tag));
+    // lanes take the queries in Morton order and write each result in place
+    PM_HIP_TRY(launch_gather(m, Q.dense, Q.n, res, s, tag, Q.perm.p));
   }
-  k_unpermute_q<<<grid_for(Q.n, 256), 256, 0, s>>>(Q.rs.p, Q.perm.p, Q.n, res);
-  return hipGetLastError();
+  return hipSuccess;
 }
 
 __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, PathOut O, const uint32_t* cidx, const float4* cres,
