@@ -208,11 +208,15 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
 //    re-reading their last node and their results are masked, so the step
 //    runs without exec-mask branches; only the wave-uniform insert round
 //    branches.
+//  - cut: admit d^2 <= cut (default prev_float(r2), i.e. d^2 < r2); a seeded
+//    cut-off (seed_cut) only narrows the walk, never the result.
+__device__ __forceinline__ float lean_cut(float r2) { return __uint_as_float(__float_as_uint(r2) - 1u); }
+
 template <int K, int QL>
-__device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float r2, bool valid,
+__device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float cut, bool valid,
                                               double (&list)[K], double* lq, int lstride) {
   const double sentinel =
-      __longlong_as_double((long long)((((uint64_t)__float_as_uint(r2)) << 32) + kKeyBias - 1));
+      __longlong_as_double((long long)((((uint64_t)__float_as_uint(cut)) << 32 | 0xFFFFFFFFull) + kKeyBias));
 #pragma unroll
   for (int j = 0; j < K; j++) list[j] = sentinel;
   if (n <= 0) return;   // empty map: every lane keeps the sentinel list (uniform)
@@ -326,13 +330,93 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   double list[kKNearest];
   const float R2 = kKMaxDistance * kKMaxDistance;
   if (LEAN) {
-    knn_walk_lean<kKNearest, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, R2, valid, list, lq + threadIdx.x, 256);
+    knn_walk_lean<kKNearest, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, lean_cut(R2), valid, list, lq + threadIdx.x, 256);
   } else {
     knn_walk<kKNearest, POST, QP, false, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, R2, valid, list, nullptr,
                                              lq + threadIdx.x, 256);
   }
   if (valid) {
     const v3 f = radiance(list, payload, qq.w, LEAN ? radiance_r2(list, R2) : key_d2(list[kKNearest - 1]));
+    out[i] = make_float4(f.x, f.y, f.z, 0.f);
+  }
+}
+
+// Seeded cut-off (PM_GATHER_MODE 12, default). Every kSeedStride-th query
+// in walk order is a LEADER; k_gather_lead runs the leaders with the plain
+// cut-off and keeps (position, K-th d^2). The other queries then start from a
+// cut-off that provably holds the K nearest: the leader's K points lie within
+// sqrt(t') of q', hence within sqrt(t') + |q - q'| of q (triangle inequality),
+// so at least K photons have d^2 <= that bound and the K smallest keys -- the
+// result -- are all admitted. The bound is the smaller of the two enclosing
+// leaders' and is inflated (1e-6 relative per step, 1e-5 on the square, 1e-30
+// absolute) past the rounding of the f32 d^2 on both sides; a leader whose list
+// did not fill (t' = -1) seeds nothing. The cut-off only prunes: the visited
+// set shrinks, the list and the radiance are bitwise those of the plain walk.
+constexpr int kSeedStride = 8;
+
+__device__ __forceinline__ double seed_bound(float4 lead, v3 q) {
+  if (!(lead.w >= 0.f)) return 1e300;
+  const double dx = (double)q.x - lead.x, dy = (double)q.y - lead.y, dz = (double)q.z - lead.z;
+  const double c = (sqrt((double)lead.w) + sqrt(dx * dx + dy * dy + dz * dz)) * (1.0 + 1e-6);
+  return c * c * (1.0 + 1e-5) + 1e-30;
+}
+// f32 cut-off >= bound (rounded up), capped at the plain cut-off
+__device__ __forceinline__ float seed_cut(double bound, float r2) {
+  const float plain = lean_cut(r2);
+  if (!(bound < (double)plain)) return plain;
+  float f = (float)bound;
+  if ((double)f < bound) f = __uint_as_float(__float_as_uint(f) + 1u);
+  return fminf(f, plain);
+}
+
+// leaders: lane j takes walk rank j * kSeedStride (query perm[rank])
+template <int TAG, int QL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_lead(
+    const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
+    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
+    int64_t nlead) {
+  __shared__ double lq[QL * 256];
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = j < nlead;
+  const int64_t r = j * kSeedStride;
+  const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
+  const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  double list[kKNearest];
+  const float R2 = kKMaxDistance * kKMaxDistance;
+  knn_walk_lean<kKNearest, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, lean_cut(R2), valid, list, lq + threadIdx.x, 256);
+  if (valid) {
+    const bool full = key_id(list[kKNearest - 1]) != 0xFFFFFFFFu;
+    const v3 f = radiance(list, payload, qq.w, full ? key_d2(list[kKNearest - 1]) : R2);
+    out[i] = make_float4(f.x, f.y, f.z, 0.f);
+    lead[j] = make_float4(qq.x, qq.y, qq.z, full ? key_d2(list[kKNearest - 1]) : -1.f);
+  }
+}
+
+// followers: lane t takes the t-th non-leader walk rank
+template <int TAG, int QL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_seeded(
+    const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
+    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, const float4* __restrict__ lead,
+    int64_t nlead) {
+  __shared__ double lq[QL * 256];
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
+  const bool valid = r < nq;
+  const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
+  const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const v3 q = {qq.x, qq.y, qq.z};
+  const float R2 = kKMaxDistance * kKMaxDistance;
+  float cut = lean_cut(R2);
+  if (valid) {
+    const int64_t jp = r / kSeedStride;
+    double b = seed_bound(lead[jp], q);
+    if (jp + 1 < nlead) b = fmin(b, seed_bound(lead[jp + 1], q));
+    cut = seed_cut(b, R2);
+  }
+  double list[kKNearest];
+  knn_walk_lean<kKNearest, QL>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
+  if (valid) {
+    const v3 f = radiance(list, payload, qq.w, radiance_r2(list, R2));
     out[i] = make_float4(f.x, f.y, f.z, 0.f);
   }
 }
@@ -437,7 +521,8 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
                          int tag, const uint32_t* perm) {
   if (nq <= 0) return hipSuccess;
   // A/B knob (read per launch), all variants return identical bits:
-  //  11 (default) mode 9 with the lean step (knn_walk_lean)   62.3 ms
+  //  12 (default) mode 11 behind leader-seeded cut-offs (k_gather_lead / _seeded)
+  //  11 mode 9 with the lean step (knn_walk_lean)   62.3 ms
   //   9 post-order + 8-deep LDS insert queue                  66.7 ms
   //   4 post-order, insert at once                             73.6 ms
   //   5 post-order + 4-entry VGPR queue (spills)               74.1 ms
@@ -445,10 +530,24 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   //   0 pre-order, insert at once
   // (config 3 global map; depths 4 / 6: 67.3 / 66.4 ms)
   const char* env = std::getenv("PM_GATHER_MODE");
-  const int mode = env ? std::atoi(env) : 11;
+  const int mode = env ? std::atoi(env) : 12;
   if (std::getenv("PM_GATHER_STATS")) gather_stats(m, qb, nq, mode, s, perm);
   const int g = grid_for(nq, 256);
   const int n = (int)m->n;
+  if (mode == 12 && nq > kSeedStride) {
+    const int64_t nlead = (nq + kSeedStride - 1) / kSeedStride;
+    DevBuf<float4> lead(nlead);
+    if (!lead.p) return hipErrorOutOfMemory;
+    const int gl = grid_for(nlead, 256), gf = grid_for(nq - nlead, 256);
+    if (tag == 1) {
+      k_gather_lead<1, 8><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
+      k_gather_seeded<1, 8><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
+    } else {
+      k_gather_lead<0, 8><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
+      k_gather_seeded<0, 8><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
+    }
+    return hipGetLastError();
+  }
 #define PM_WALK(P, Q, L, LEAN)                                                                          \
   (tag == 1 ? (k_gather<1, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm))  \
             : (k_gather<0, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm)))

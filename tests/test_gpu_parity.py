@@ -434,7 +434,7 @@ def test_frame_driver_matches_direct_pipeline(cornell):
         assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("mode", ["0", "4", "5", "10", "11"])
+@pytest.mark.parametrize("mode", ["0", "4", "5", "9", "10", "11", "12"])
 def test_gather_modes_bitwise(cornell, monkeypatch, mode):
     """Every PM_GATHER_MODE walk returns the default gather's bits (pm_gather
     and a render), incl. on an empty map."""
@@ -481,3 +481,29 @@ def test_render_continuation_rerun(sphere, monkeypatch):
     assert pm_amd.render_stats().path_vertices > W * H * 2   # continuation vertices existed
     assert torch.equal(a, b)
     assert np.array_equal(_bits(ra.cpu().numpy()), _bits(rb.cpu().numpy()))
+
+
+@pytest.mark.parametrize("jitter", [0.0, 1e-3, 0.5])
+def test_seeded_gather_tight_neighbours(cornell, monkeypatch, jitter):
+    """Mode 12 (leader-seeded cut-offs) on queries in spatial order, where the
+    leader bounds are tight: queries at photon positions (d^2 = 0 ties),
+    duplicated queries and small jitters. Bitwise equal to the plain walk."""
+    import pm_amd
+    meshes, lights = cornell
+    gs = pm_amd.Scene(meshes)
+    g = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, False)
+    c = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, True)
+    gm, cm = pm_amd.load_photons(g, c)
+    rng = np.random.default_rng(11)
+    gn = g.cpu().numpy()
+    q = gn[rng.integers(0, len(gn), 6000), 0:3].astype(np.float32)
+    q = np.concatenate([q, q[:500]])   # exact duplicates
+    q = q + (rng.normal(scale=jitter, size=q.shape).astype(np.float32) if jitter else 0)
+    q = q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))].astype(np.float32)
+    qt = torch.from_numpy(np.ascontiguousarray(q)).cuda()
+    brdf = torch.from_numpy(rng.uniform(0, 0.4, size=len(q)).astype(np.float32)).cuda()
+    monkeypatch.setenv("PM_GATHER_MODE", "11")
+    ref = [pm_amd.gather_photons(m, qt, brdf).cpu().numpy() for m in (gm, cm)]
+    monkeypatch.setenv("PM_GATHER_MODE", "12")
+    for m, r in zip((gm, cm), ref):
+        assert np.array_equal(_bits(pm_amd.gather_photons(m, qt, brdf).cpu().numpy()), _bits(r))
