@@ -15,6 +15,7 @@
 // whenever any lane inserts: it is built from v_min_f64 / v_max_f64 only
 // (list_insert), and the walk tests a node's point post-order so root-path
 // points meet a tight bound (knn_walk<POST = true>; variants: DESIGN.md §4.4).
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 
@@ -212,7 +213,15 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
 //    cut-off (seed_cut) only narrows the walk, never the result.
 __device__ __forceinline__ float lean_cut(float r2) { return __uint_as_float(__float_as_uint(r2) - 1u); }
 
-template <int K, int QL>
+//  - JUMP: finished subtrees are left without re-reading the nodes above them.
+//    A per-lane bit mask records, per depth, whether the path entered that
+//    depth's node as the FAR child. A node whose far child is done (or
+//    skipped) is finished; so is every consecutive far-child ancestor, whose
+//    far child it was. The walk jumps straight to the parent of the deepest
+//    close-child ancestor-or-self (one step, one cached load), where the
+//    post-order point test and the far decision run. Same visited set, same
+//    point tests, fewer dependent loads.
+template <int K, int QL, bool JUMP = false>
 __device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float cut, bool valid,
                                               double (&list)[K], double* lq, int lstride) {
   const double sentinel =
@@ -222,6 +231,8 @@ __device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, 
   if (n <= 0) return;   // empty map: every lane keeps the sentinel list (uniform)
   float bound = key_d2(sentinel);
   int prev = -1, curr = 0;
+  uint32_t far_mask = 0;   // JUMP: bit d set <=> the path's depth-d node is a far child
+  int depth = 0;           // JUMP: depth of curr
   bool walking = valid;
   int qn = 0;
   for (;;) {
@@ -239,14 +250,38 @@ __device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, 
     const float d2 = dx * dx + dy * dy + dz * dz;
     const double key = key_make(d2, (uint32_t)(w >> 2));
     const bool cand = walking && test && key < list[K - 1];
-    int next;
-    if (prev == far_c) next = parent;
-    else if (prev == close_c || close_c >= n) next = (far_c < n && diff * diff <= bound) ? far_c : parent;
-    else next = close_c;
+    int next, nprev;
+    if (JUMP) {
+      if (down && close_c < n) {
+        next = close_c;
+        nprev = curr;
+        far_mask &= ~(2u << depth);
+        depth++;
+      } else if (far_c < n && diff * diff <= bound) {
+        next = far_c;
+        nprev = curr;
+        far_mask |= 2u << depth;
+        depth++;
+      } else {
+        // curr is finished: deepest close-child ancestor-or-self a (depth da);
+        // bit 0 (the root) is always clear, so da = 0 ends the walk
+        const uint32_t open = (~far_mask & ((2u << depth) - 1u)) | 1u;
+        const int da = 31 - __clz(open);
+        const int a = ((curr + 1) >> (depth - da)) - 1;
+        next = da == 0 ? -1 : ((a + 1) >> 1) - 1;
+        nprev = a;
+        depth = da - 1;
+      }
+    } else {
+      if (prev == far_c) next = parent;
+      else if (prev == close_c || close_c >= n) next = (far_c < n && diff * diff <= bound) ? far_c : parent;
+      else next = close_c;
+      nprev = curr;
+    }
     lq[qn * lstride] = key;
     qn += cand ? 1 : 0;
     const bool go = walking && next >= 0;
-    prev = go ? curr : prev;
+    prev = go ? nprev : prev;
     curr = go ? next : curr;
     walking = go;
     const bool any_walking = __ballot(walking) != 0;
@@ -315,7 +350,7 @@ __device__ __forceinline__ v3 radiance(const double (&list)[kKNearest], const fl
 // TAG only separates the global-map launch into its own kernel symbol (rocprof).
 // perm (optional): lane i takes query perm[i] and writes its result there, so a
 // caller can walk in Morton order without permuted / unpermuted copies.
-template <int TAG, bool POST, int QP, int QL = 0, bool LEAN = false>
+template <int TAG, bool POST, int QP, int QL = 0, bool LEAN = false, bool JUMP = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm) {
@@ -330,7 +365,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   double list[kKNearest];
   const float R2 = kKMaxDistance * kKMaxDistance;
   if (LEAN) {
-    knn_walk_lean<kKNearest, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, lean_cut(R2), valid, list, lq + threadIdx.x, 256);
+    knn_walk_lean<kKNearest, QL, JUMP>(nodes, n, v3{qq.x, qq.y, qq.z}, lean_cut(R2), valid, list, lq + threadIdx.x,
+                                       256);
   } else {
     knn_walk<kKNearest, POST, QP, false, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, R2, valid, list, nullptr,
                                              lq + threadIdx.x, 256);
@@ -370,7 +406,7 @@ __device__ __forceinline__ float seed_cut(double bound, float r2) {
 }
 
 // leaders: lane j takes walk rank j * kSeedStride (query perm[rank])
-template <int TAG, int QL>
+template <int TAG, int QL, bool JUMP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_lead(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
@@ -383,7 +419,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   double list[kKNearest];
   const float R2 = kKMaxDistance * kKMaxDistance;
-  knn_walk_lean<kKNearest, QL>(nodes, n, v3{qq.x, qq.y, qq.z}, lean_cut(R2), valid, list, lq + threadIdx.x, 256);
+  knn_walk_lean<kKNearest, QL, JUMP>(nodes, n, v3{qq.x, qq.y, qq.z}, lean_cut(R2), valid, list, lq + threadIdx.x,
+                                     256);
   if (valid) {
     const bool full = key_id(list[kKNearest - 1]) != 0xFFFFFFFFu;
     const v3 f = radiance(list, payload, qq.w, full ? key_d2(list[kKNearest - 1]) : R2);
@@ -393,7 +430,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 // followers: lane t takes the t-th non-leader walk rank
-template <int TAG, int QL>
+template <int TAG, int QL, bool JUMP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_seeded(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, const float4* __restrict__ lead,
@@ -414,10 +451,95 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     cut = seed_cut(b, R2);
   }
   double list[kKNearest];
-  knn_walk_lean<kKNearest, QL>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
+  knn_walk_lean<kKNearest, QL, JUMP>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
   if (valid) {
     const v3 f = radiance(list, payload, qq.w, radiance_r2(list, R2));
     out[i] = make_float4(f.x, f.y, f.z, 0.f);
+  }
+}
+
+// Diagnostic (PM_GATHER_MODE 16): pass 1 records each query's exact K-th d^2,
+// pass 2 (k_gather_exactcut) re-walks from that cut-off: the floor any seeded
+// cut-off can reach.
+template <int TAG, bool JUMP, bool SECOND>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_exactcut(
+    const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
+    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float* __restrict__ cutb) {
+  __shared__ double lq[8 * 256];
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = r < nq;
+  const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
+  const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float R2 = kKMaxDistance * kKMaxDistance;
+  const float cut = (SECOND && valid) ? cutb[r] : lean_cut(R2);
+  double list[kKNearest];
+  knn_walk_lean<kKNearest, 8, JUMP>(nodes, n, v3{qq.x, qq.y, qq.z}, cut, valid, list, lq + threadIdx.x, 256);
+  if (valid) {
+    const v3 f = radiance(list, payload, qq.w, radiance_r2(list, R2));
+    out[i] = make_float4(f.x, f.y, f.z, 0.f);
+    if (!SECOND) cutb[r] = key_id(list[kKNearest - 1]) != 0xFFFFFFFFu ? key_d2(list[kKNearest - 1]) : lean_cut(R2);
+  }
+}
+
+// Diagnostic (PM_GATHER_SEEDSTATS=1): how tight seeded cut-offs are. For each
+// query with a full list: the bound from the query d places earlier in walk
+// order (d = 1, 2, 4), and the production stride-8 two-leader bound, each
+// divided by the query's exact K-th d^2; histogram of log2(ratio) in 1/4 steps.
+__global__ void k_seed_stats(const float4* __restrict__ qb, int64_t nq, const uint32_t* __restrict__ perm,
+                             const float* __restrict__ cutb, unsigned long long* hist) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nq || r < 8) return;
+  const float4 qq = qb[perm ? perm[r] : r];
+  const v3 q = {qq.x, qq.y, qq.z};
+  const float ex = cutb[r];
+  if (!(ex > 0.f) || ex >= 9999.f) return;
+  auto bin = [&](double b) {
+    const double l = log2(b / ex) * 4.0;
+    return (int)fmin(fmax(l, 0.0), 31.0);
+  };
+  const int ds[3] = {1, 2, 4};
+  for (int k = 0; k < 3; k++) {
+    const int64_t o = r - ds[k];
+    const float4 p = qb[perm ? perm[o] : o];
+    const double b = seed_bound(make_float4(p.x, p.y, p.z, cutb[o] < 9999.f ? cutb[o] : -1.f), q);
+    atomicAdd(&hist[k * 32 + bin(b)], 1ull);
+  }
+  if (r % kSeedStride) {
+    const int64_t l0 = r - r % kSeedStride, l1 = l0 + kSeedStride;
+    const float4 p0 = qb[perm ? perm[l0] : l0];
+    double b = seed_bound(make_float4(p0.x, p0.y, p0.z, cutb[l0] < 9999.f ? cutb[l0] : -1.f), q);
+    if (l1 < nq) {
+      const float4 p1 = qb[perm ? perm[l1] : l1];
+      b = fmin(b, seed_bound(make_float4(p1.x, p1.y, p1.z, cutb[l1] < 9999.f ? cutb[l1] : -1.f), q));
+    }
+    atomicAdd(&hist[3 * 32 + bin(b)], 1ull);
+  }
+}
+
+static void seed_stats(const pm_photon_map* m, const float4* qb, int64_t nq, hipStream_t s, const uint32_t* perm) {
+  DevBuf<float> cutb(nq);
+  DevBuf<float4> tmp(nq);
+  DevBuf<unsigned long long> hist(128);
+  if (!cutb.p || !tmp.p || !hist.p || hipMemsetAsync(hist.p, 0, 128 * 8, s) != hipSuccess) return;
+  const int g = grid_for(nq, 256);
+  k_gather_exactcut<0, true, false><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, (int)m->n, qb, nq, tmp.p, perm,
+                                                       cutb.p);
+  k_seed_stats<<<g, 256, 0, s>>>(qb, nq, perm, cutb.p, hist.p);
+  unsigned long long h[128] = {};
+  if (hipMemcpyAsync(h, hist.p, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return;
+  const char* names[4] = {"prev 1", "prev 2", "prev 4", "stride-8 leaders"};
+  for (int k = 0; k < 4; k++) {
+    double tot = 0, mean = 0;
+    for (int b = 0; b < 32; b++) tot += (double)h[k * 32 + b];
+    std::fprintf(stderr, "[seed-stats n=%lld nq=%lld] %-16s log2(bound/exact)*4 hist:", (long long)m->n,
+                 (long long)nq, names[k]);
+    for (int b = 0; b < 32; b++) {
+      mean += (double)h[k * 32 + b] * std::exp2((b + 0.5) / 4.0);
+      std::fprintf(stderr, " %.3f", tot > 0 ? h[k * 32 + b] / tot : 0.0);
+    }
+    std::fprintf(stderr, " | mean ratio ~%.2f\n", tot > 0 ? mean / tot : 0.0);
   }
 }
 
@@ -521,7 +643,10 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
                          int tag, const uint32_t* perm) {
   if (nq <= 0) return hipSuccess;
   // A/B knob (read per launch), all variants return identical bits:
-  //  12 (default) mode 11 behind leader-seeded cut-offs (k_gather_lead / _seeded)
+  //  13 (default) mode 12 with the JUMP walk                   50.9 ms
+  //  14 mode 11 with the JUMP walk                             59.0 ms
+  //  16 / 17 diagnostic: exact-cut re-walk (JUMP / plain), see k_gather_exactcut
+  //  12 mode 11 behind leader-seeded cut-offs (k_gather_lead / _seeded)   53.5 ms
   //  11 mode 9 with the lean step (knn_walk_lean)   62.3 ms
   //   9 post-order + 8-deep LDS insert queue                  66.7 ms
   //   4 post-order, insert at once                             73.6 ms
@@ -530,29 +655,44 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   //   0 pre-order, insert at once
   // (config 3 global map; depths 4 / 6: 67.3 / 66.4 ms)
   const char* env = std::getenv("PM_GATHER_MODE");
-  const int mode = env ? std::atoi(env) : 12;
+  const int mode = env ? std::atoi(env) : 13;
   if (std::getenv("PM_GATHER_STATS")) gather_stats(m, qb, nq, mode, s, perm);
+  if (std::getenv("PM_GATHER_SEEDSTATS")) seed_stats(m, qb, nq, s, perm);
   const int g = grid_for(nq, 256);
   const int n = (int)m->n;
-  if (mode == 12 && nq > kSeedStride) {
+  if ((mode == 12 || mode == 13) && nq > kSeedStride) {
     const int64_t nlead = (nq + kSeedStride - 1) / kSeedStride;
     DevBuf<float4> lead(nlead);
     if (!lead.p) return hipErrorOutOfMemory;
     const int gl = grid_for(nlead, 256), gf = grid_for(nq - nlead, 256);
-    if (tag == 1) {
-      k_gather_lead<1, 8><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
-      k_gather_seeded<1, 8><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
+#define PM_SEEDED(T, J)                                                                                     \
+  k_gather_lead<T, 8, J><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead); \
+  k_gather_seeded<T, 8, J><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
+    if (tag == 1 && mode == 13) { PM_SEEDED(1, true) }
+    else if (tag == 1) { PM_SEEDED(1, false) }
+    else if (mode == 13) { PM_SEEDED(0, true) }
+    else { PM_SEEDED(0, false) }
+#undef PM_SEEDED
+    return hipGetLastError();
+  }
+  if (mode == 16 || mode == 17) {
+    DevBuf<float> cutb(nq);
+    if (!cutb.p) return hipErrorOutOfMemory;
+    if (mode == 16) {
+      k_gather_exactcut<0, true, false><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, cutb.p);
+      k_gather_exactcut<1, true, true><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, cutb.p);
     } else {
-      k_gather_lead<0, 8><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
-      k_gather_seeded<0, 8><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
+      k_gather_exactcut<0, false, false><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, cutb.p);
+      k_gather_exactcut<1, false, true><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, cutb.p);
     }
     return hipGetLastError();
   }
-#define PM_WALK(P, Q, L, LEAN)                                                                          \
-  (tag == 1 ? (k_gather<1, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm))  \
-            : (k_gather<0, P, Q, L, LEAN><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm)))
+#define PM_WALK(P, Q, L, LEAN, ...)                                                                                  \
+  (tag == 1 ? (k_gather<1, P, Q, L, LEAN, ##__VA_ARGS__><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm)) \
+            : (k_gather<0, P, Q, L, LEAN, ##__VA_ARGS__><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm)))
   switch (mode) {
     case 11: PM_WALK(true, 0, 8, true); break;
+    case 14: PM_WALK(true, 0, 8, true, true); break;
     case 0: PM_WALK(false, 0, 0, false); break;
     case 4: PM_WALK(true, 0, 0, false); break;
     case 5: PM_WALK(true, 4, 0, false); break;

@@ -434,7 +434,7 @@ def test_frame_driver_matches_direct_pipeline(cornell):
         assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("mode", ["0", "4", "5", "9", "10", "11", "12"])
+@pytest.mark.parametrize("mode", ["0", "4", "5", "9", "10", "11", "12", "13", "14"])
 def test_gather_modes_bitwise(cornell, monkeypatch, mode):
     """Every PM_GATHER_MODE walk returns the default gather's bits (pm_gather
     and a render), incl. on an empty map."""
@@ -504,6 +504,7 @@ def test_seeded_gather_tight_neighbours(cornell, monkeypatch, jitter):
     brdf = torch.from_numpy(rng.uniform(0, 0.4, size=len(q)).astype(np.float32)).cuda()
     monkeypatch.setenv("PM_GATHER_MODE", "11")
     ref = [pm_amd.gather_photons(m, qt, brdf).cpu().numpy() for m in (gm, cm)]
-    monkeypatch.setenv("PM_GATHER_MODE", "12")
-    for m, r in zip((gm, cm), ref):
-        assert np.array_equal(_bits(pm_amd.gather_photons(m, qt, brdf).cpu().numpy()), _bits(r))
+    for mode in ("12", "13", "14"):
+        monkeypatch.setenv("PM_GATHER_MODE", mode)
+        for m, r in zip((gm, cm), ref):
+            assert np.array_equal(_bits(pm_amd.gather_photons(m, qt, brdf).cpu().numpy()), _bits(r)), mode
