@@ -377,18 +377,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   }
 }
 
-// Seeded cut-off (PM_GATHER_MODE 12, default). Every kSeedStride-th query
+// Seeded cut-off (PM_GATHER_MODE 12; 13 = with the JUMP walk, default). Every kSeedStride-th query
 // in walk order is a LEADER; k_gather_lead runs the leaders with the plain
 // cut-off and keeps (position, K-th d^2). The other queries then start from a
 // cut-off that provably holds the K nearest: the leader's K points lie within
 // sqrt(t') of q', hence within sqrt(t') + |q - q'| of q (triangle inequality),
 // so at least K photons have d^2 <= that bound and the K smallest keys -- the
-// result -- are all admitted. The bound is the smaller of the two enclosing
+// result -- are all admitted. The bound is the smallest over the consulted
 // leaders' and is inflated (1e-6 relative per step, 1e-5 on the square, 1e-30
 // absolute) past the rounding of the f32 d^2 on both sides; a leader whose list
 // did not fill (t' = -1) seeds nothing. The cut-off only prunes: the visited
 // set shrinks, the list and the radiance are bitwise those of the plain walk.
-constexpr int kSeedStride = 8;
+// Leader stride and leaders consulted per follower (the enclosing pair, plus one
+// more on each side): build knobs. Config 3 global gather (ms): stride 8 / 2
+// leaders 50.9, 8/4 50.3, 4/2 52.2, 16/2 50.6, 16/4 49.8. A follower bound from
+// the union of the enclosing leaders' neighbour sets (K-th smallest distance,
+// exact by construction) was tighter but slower: 54.6 (its 1.6 KB of leader
+// points per follower cost more than the walk saved).
+#ifndef PM_SEED_STRIDE
+#define PM_SEED_STRIDE 16
+#endif
+#ifndef PM_SEED_LEADERS
+#define PM_SEED_LEADERS 4
+#endif
+constexpr int kSeedStride = PM_SEED_STRIDE;
 
 __device__ __forceinline__ double seed_bound(float4 lead, v3 q) {
   if (!(lead.w >= 0.f)) return 1e300;
@@ -448,6 +460,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int64_t jp = r / kSeedStride;
     double b = seed_bound(lead[jp], q);
     if (jp + 1 < nlead) b = fmin(b, seed_bound(lead[jp + 1], q));
+    if (PM_SEED_LEADERS > 2) {
+      if (jp >= 1) b = fmin(b, seed_bound(lead[jp - 1], q));
+      if (jp + 2 < nlead) b = fmin(b, seed_bound(lead[jp + 2], q));
+    }
     cut = seed_cut(b, R2);
   }
   double list[kKNearest];
