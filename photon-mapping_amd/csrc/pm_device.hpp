@@ -337,6 +337,10 @@ __device__ __forceinline__ bool leaf_test(const DevScene& S, const Ray& r, float
 #ifndef PM_LEAF_BATCH
 #define PM_LEAF_BATCH 1
 #endif
+// PM_LEAF_COMPACT (build knob): test the hit leaves in compacted rounds.
+#ifndef PM_LEAF_COMPACT
+#define PM_LEAF_COMPACT 1
+#endif
 template <bool ANY, int NB>
 __device__ __forceinline__ bool leaf_batch(const DevScene& S, const Ray& r, float tmin, float tmax, const bool (&lv)[NB],
                                            const int (&code)[NB], HitInfo& h) {
@@ -356,6 +360,93 @@ __device__ __forceinline__ bool leaf_batch(const DevScene& S, const Ray& r, floa
   return false;
 }
 
+// One traversal step: visit `node` (slab-test its 4 children, test its leaf
+// children, push the internal hits near-to-far and continue with the nearest,
+// or pop). Returns true when the ray is finished (stack empty, or an any-hit).
+template <bool ANY>
+__device__ __forceinline__ bool traverse_step(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
+                                              int stride, int* spill, int& node, int& sp, HitInfo& h,
+                                              int* overflow) {
+  const float4* q = S.nodes + 8 * (int64_t)node;
+  const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+  const int4 ch = *reinterpret_cast<const int4*>(&q[6]);
+  const float lim = (ANY || h.slot < 0) ? tmax * 1.00001f : h.t * 1.00001f;
+  float t0, t1, t2, t3;
+  const bool b0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, tmin, lim, t0) && ch.x != kBvhEmpty;
+  const bool b1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tmin, lim, t1) && ch.y != kBvhEmpty;
+  const bool b2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tmin, lim, t2) && ch.z != kBvhEmpty;
+  const bool b3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tmin, lim, t3) && ch.w != kBvhEmpty;
+  // leaves first: a hit shrinks the limit applied to the internal children
+  if (PM_LEAF_BATCH == 4) {
+    const bool lv[4] = {b0 && ch.x < 0, b1 && ch.y < 0, b2 && ch.z < 0, b3 && ch.w < 0};
+    const int cd[4] = {ch.x, ch.y, ch.z, ch.w};
+    if (leaf_batch<ANY, 4>(S, r, tmin, tmax, lv, cd, h)) return true;
+  } else if (PM_LEAF_BATCH == 2) {
+    const bool lv0[2] = {b0 && ch.x < 0, b1 && ch.y < 0}, lv1[2] = {b2 && ch.z < 0, b3 && ch.w < 0};
+    const int cd0[2] = {ch.x, ch.y}, cd1[2] = {ch.z, ch.w};
+    if (leaf_batch<ANY, 2>(S, r, tmin, tmax, lv0, cd0, h)) return true;
+    if (leaf_batch<ANY, 2>(S, r, tmin, tmax, lv1, cd1, h)) return true;
+  } else if (PM_LEAF_COMPACT) {
+    // hit leaves compacted to the front: round k tests every lane's k-th hit
+    // leaf, and the wave runs max(#hit leaves) rounds (order-free: argmin)
+    const bool f0 = b0 && ch.x < 0, f1 = b1 && ch.y < 0, f2 = b2 && ch.z < 0, f3 = b3 && ch.w < 0;
+    int l0 = f0 ? ch.x : (f1 ? ch.y : (f2 ? ch.z : ch.w));
+    int l1 = (f0 && f1) ? ch.y : ((f0 || f1) && f2 ? ch.z : ch.w);
+    int l2 = (f0 + f1 + f2 == 3) ? ch.z : ch.w;
+    const int nl = f0 + f1 + f2 + f3;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (__ballot(k < nl) == 0) break;
+      const int c = k == 0 ? l0 : (k == 1 ? l1 : (k == 2 ? l2 : ch.w));
+      if (k < nl && leaf_test<ANY>(S, r, tmin, tmax, c, h) && ANY) return true;
+    }
+  } else {
+    if (b0 && ch.x < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.x, h) && ANY) return true;
+    if (b1 && ch.y < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.y, h) && ANY) return true;
+    if (b2 && ch.z < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.z, h) && ANY) return true;
+    if (b3 && ch.w < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.w, h) && ANY) return true;
+  }
+  const float lim2 = (ANY || h.slot < 0) ? lim : h.t * 1.00001f;
+  // internal children hit within the (possibly tightened) limit, sorted
+  // near-to-far: order only changes speed, the result is argmin (t, id)
+  float k0 = (b0 && ch.x >= 0 && t0 <= lim2) ? t0 : INFINITY;
+  float k1 = (b1 && ch.y >= 0 && t1 <= lim2) ? t1 : INFINITY;
+  float k2 = (b2 && ch.z >= 0 && t2 <= lim2) ? t2 : INFINITY;
+  float k3 = (b3 && ch.w >= 0 && t3 <= lim2) ? t3 : INFINITY;
+  const int cnt = (k0 != INFINITY) + (k1 != INFINITY) + (k2 != INFINITY) + (k3 != INFINITY);
+  int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+  cas(k0, c0, k1, c1);
+  cas(k2, c2, k3, c3);
+  cas(k0, c0, k2, c2);
+  cas(k1, c1, k3, c3);
+  cas(k1, c1, k2, c2);
+  if (cnt > 0) {
+    if (sp + cnt - 1 > kStackDepth + kSpillDepth) {
+      *overflow = 1;
+    } else if (sp + cnt - 1 <= kStackDepth) {
+      if (cnt > 3) stack[(sp++) * stride] = c3;
+      if (cnt > 2) stack[(sp++) * stride] = c2;
+      if (cnt > 1) stack[(sp++) * stride] = c1;
+    } else if (kSpillDepth > 0) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const int c = k == 0 ? c3 : (k == 1 ? c2 : c1);
+        if (k >= 4 - cnt) {
+          if (sp < kStackDepth) stack[sp * stride] = c;
+          else spill[sp - kStackDepth] = c;
+          sp++;
+        }
+      }
+    }
+    node = c0;
+    return false;
+  }
+  if (sp == 0) return true;
+  sp--;
+  node = (kSpillDepth == 0 || sp < kStackDepth) ? stack[sp * stride] : spill[sp - kStackDepth];
+  return false;
+}
+
 template <bool ANY>
 __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
                                             int stride, int* overflow) {
@@ -364,72 +455,77 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
   int spill[kSpillDepth > 0 ? kSpillDepth : 1];
   int sp = 0;
   int node = 0;
+  while (!traverse_step<ANY>(S, r, tmin, tmax, stack, stride, spill, node, sp, h, overflow)) {
+  }
+  return h;
+}
+
+// Chunked ray pool: workgroup b traces rays [b*chunk, (b+1)*chunk) of n. A lane
+// whose ray is finished takes the chunk's next ray, so a wave keeps its lanes
+// busy instead of idling until its slowest ray is done (one ray per lane left
+// ~80 % of the VALU lanes idle in the traversal kernels). Idle lanes are
+// refilled together (one LDS atomic per wave) once kPoolRefill of them wait.
+// fetch(i, Ray&, tmin&, tmax&) -> false skips ray i; done(i, Ray, HitInfo)
+// consumes a result. `lnext` is an LDS counter zeroed before the call (block
+// barrier); every wave exits once the chunk is drained and its lanes are done.
+// pool_chunk picks the chunk: up to PM_POOL_RAYS rays per lane, fewer when the
+// launch would otherwise have fewer than ~16 workgroups per CU.
+#ifndef PM_POOL_RAYS
+#define PM_POOL_RAYS 8
+#endif
+inline int pool_chunk(int64_t n, int block) {
+  const int64_t target = 256 * 16;   // workgroups: 256 CUs x 16
+  int64_t per = (n + target * block - 1) / (target * block);
+  per = per < 1 ? 1 : (per > PM_POOL_RAYS ? PM_POOL_RAYS : per);
+  return (int)(per * block);
+}
+#ifndef PM_POOL_REFILL
+#define PM_POOL_REFILL 16
+#endif
+template <bool ANY, typename Fetch, typename Done>
+__device__ __forceinline__ void traverse_pool(const DevScene& S, int* stack, int stride, int* overflow, int64_t n,
+                                              int chunk, int* lnext, Fetch fetch, Done done) {
+  const int64_t cbase = (int64_t)blockIdx.x * chunk;
+  const int cn = (int)(n - cbase < chunk ? n - cbase : chunk);
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int spill[kSpillDepth > 0 ? kSpillDepth : 1];
+  Ray r;
+  float tmin = 0.f, tmax = 0.f;
+  HitInfo h{0.f, -1, -1};
+  int node = 0, sp = 0, cur = -1;
+  bool drained = false;
   for (;;) {
-    const float4* q = S.nodes + 8 * (int64_t)node;
-    const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
-    const int4 ch = *reinterpret_cast<const int4*>(&q[6]);
-    const float lim = (ANY || h.slot < 0) ? tmax * 1.00001f : h.t * 1.00001f;
-    float t0, t1, t2, t3;
-    const bool b0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, tmin, lim, t0) && ch.x != kBvhEmpty;
-    const bool b1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tmin, lim, t1) && ch.y != kBvhEmpty;
-    const bool b2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tmin, lim, t2) && ch.z != kBvhEmpty;
-    const bool b3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tmin, lim, t3) && ch.w != kBvhEmpty;
-    // leaves first: a hit shrinks the limit applied to the internal children
-    if (PM_LEAF_BATCH == 4) {
-      const bool lv[4] = {b0 && ch.x < 0, b1 && ch.y < 0, b2 && ch.z < 0, b3 && ch.w < 0};
-      const int cd[4] = {ch.x, ch.y, ch.z, ch.w};
-      if (leaf_batch<ANY, 4>(S, r, tmin, tmax, lv, cd, h)) return h;
-    } else if (PM_LEAF_BATCH == 2) {
-      const bool lv0[2] = {b0 && ch.x < 0, b1 && ch.y < 0}, lv1[2] = {b2 && ch.z < 0, b3 && ch.w < 0};
-      const int cd0[2] = {ch.x, ch.y}, cd1[2] = {ch.z, ch.w};
-      if (leaf_batch<ANY, 2>(S, r, tmin, tmax, lv0, cd0, h)) return h;
-      if (leaf_batch<ANY, 2>(S, r, tmin, tmax, lv1, cd1, h)) return h;
-    } else {
-      if (b0 && ch.x < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.x, h) && ANY) return h;
-      if (b1 && ch.y < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.y, h) && ANY) return h;
-      if (b2 && ch.z < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.z, h) && ANY) return h;
-      if (b3 && ch.w < 0 && leaf_test<ANY>(S, r, tmin, tmax, ch.w, h) && ANY) return h;
-    }
-    const float lim2 = (ANY || h.slot < 0) ? lim : h.t * 1.00001f;
-    // internal children hit within the (possibly tightened) limit, sorted
-    // near-to-far: order only changes speed, the result is argmin (t, id)
-    float k0 = (b0 && ch.x >= 0 && t0 <= lim2) ? t0 : INFINITY;
-    float k1 = (b1 && ch.y >= 0 && t1 <= lim2) ? t1 : INFINITY;
-    float k2 = (b2 && ch.z >= 0 && t2 <= lim2) ? t2 : INFINITY;
-    float k3 = (b3 && ch.w >= 0 && t3 <= lim2) ? t3 : INFINITY;
-    const int cnt = (k0 != INFINITY) + (k1 != INFINITY) + (k2 != INFINITY) + (k3 != INFINITY);
-    int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-    cas(k0, c0, k1, c1);
-    cas(k2, c2, k3, c3);
-    cas(k0, c0, k2, c2);
-    cas(k1, c1, k3, c3);
-    cas(k1, c1, k2, c2);
-    if (cnt > 0) {
-      if (sp + cnt - 1 > kStackDepth + kSpillDepth) {
-        *overflow = 1;
-      } else if (sp + cnt - 1 <= kStackDepth) {
-        if (cnt > 3) stack[(sp++) * stride] = c3;
-        if (cnt > 2) stack[(sp++) * stride] = c2;
-        if (cnt > 1) stack[(sp++) * stride] = c1;
-      } else if (kSpillDepth > 0) {
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-          const int c = k == 0 ? c3 : (k == 1 ? c2 : c1);
-          if (k >= 4 - cnt) {
-            if (sp < kStackDepth) stack[sp * stride] = c;
-            else spill[sp - kStackDepth] = c;
-            sp++;
+    const uint64_t idle = __ballot(cur < 0);
+    const int nidle = __popcll(idle);
+    if (!drained && nidle >= PM_POOL_REFILL) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(lnext, nidle);
+      base = __shfl(base, 0);
+      if (base + nidle >= cn) drained = true;
+      if (cur < 0) {
+        const int idx = base + __popcll(idle & lt_mask);
+        if (idx < cn && fetch(cbase + idx, r, tmin, tmax)) {
+          cur = idx;
+          h = HitInfo{tmax, -1, -1};
+          node = 0;
+          sp = 0;
+          if (S.ntri <= 0) {   // empty scene: miss at once
+            done(cbase + cur, r, h);
+            cur = -1;
           }
         }
       }
-      node = c0;
+    }
+    if (__ballot(cur >= 0) == 0) {
+      if (drained) break;
       continue;
     }
-    if (sp == 0) break;
-    sp--;
-    node = (kSpillDepth == 0 || sp < kStackDepth) ? stack[sp * stride] : spill[sp - kStackDepth];
+    if (cur >= 0 && traverse_step<ANY>(S, r, tmin, tmax, stack, stride, spill, node, sp, h, overflow)) {
+      done(cbase + cur, r, h);
+      cur = -1;
+    }
   }
-  return h;
 }
 
 // 30-bit Morton code of a point inside the box (lo, 1 / extent): only used to

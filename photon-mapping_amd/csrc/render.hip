@@ -330,6 +330,66 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_RAYS_WAVES) void k_shadow
   svis[si] = h.slot >= 0 ? 0u : 1u;
 }
 
+// Ray-pool versions of k_diffuse_rays / k_shadow_rays (PM_RAY_POOL, see
+// traverse_pool): same per-ray results.
+#ifndef PM_RAY_POOL
+#define PM_RAY_POOL 1
+#endif
+__global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_RAYS_WAVES) void k_diffuse_rays_pool(
+    DevScene S, const float4* __restrict__ cq, const float4* __restrict__ gdir, int64_t ng,
+    uint32_t* __restrict__ gvalid, float4* __restrict__ gq, float4* __restrict__ galb, int* overflow, int chunk) {
+  __shared__ int stack[kStackDepth * kRBlock];
+  __shared__ int lnext;
+  if (threadIdx.x == 0) lnext = 0;
+  __syncthreads();
+  traverse_pool<false>(
+      S, stack + threadIdx.x, kRBlock, overflow, ng, chunk, &lnext,
+      [&](int64_t gi, Ray& r, float& tmin, float& tmax) {
+        if (!gvalid[gi]) return false;
+        const float4 c = cq[gi / kNumDiffuseSamples];
+        const float4 dd = gdir[gi];
+        ray_prep(r, v3{c.x, c.y, c.z}, v3{dd.x, dd.y, dd.z});
+        tmin = 3 * kEPS;
+        tmax = kINFTY;
+        return true;
+      },
+      [&](int64_t gi, const Ray& r, const HitInfo& h) {
+        uint32_t ok = 0;
+        if (h.slot >= 0) {
+          const int mesh = __float_as_int(S.tri[3 * h.slot].w);
+          const float4 m0 = S.mat[2 * mesh];
+          if (m0.w > 0.f) {
+            const v3 hp = add(r.o, mulf(r.d, h.t));
+            gq[gi] = make_float4(hp.x, hp.y, hp.z, m0.w / kPI);
+            galb[gi] = make_float4(m0.x, m0.y, m0.z, 0.f);
+            ok = 1;
+          }
+        }
+        gvalid[gi] = ok;
+      });
+}
+
+__global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_RAYS_WAVES) void k_shadow_rays_pool(
+    DevScene S, const float4* __restrict__ cq, const float4* __restrict__ sray, int nl, int64_t ns,
+    uint32_t* __restrict__ svis, int* overflow, int chunk) {
+  __shared__ int stack[kStackDepth * kRBlock];
+  __shared__ int lnext;
+  if (threadIdx.x == 0) lnext = 0;
+  __syncthreads();
+  traverse_pool<true>(
+      S, stack + threadIdx.x, kRBlock, overflow, ns, chunk, &lnext,
+      [&](int64_t si, Ray& r, float& tmin, float& tmax) {
+        const float4 sr = sray[si];
+        if (sr.w < 0.f) return false;
+        const float4 c = cq[si / nl];
+        ray_prep(r, v3{c.x, c.y, c.z}, v3{sr.x, sr.y, sr.z});
+        tmin = kEPS;
+        tmax = sr.w;
+        return true;
+      },
+      [&](int64_t si, const Ray&, const HitInfo& h) { svis[si] = h.slot >= 0 ? 0u : 1u; });
+}
+
 // Direct light of each hit vertex, summed over the lights in order exactly as
 // deviceCode.cu:145-171 (vis * power * ldn * inv * brdf * rgb), times albedo.
 __global__ __launch_bounds__(256) void k_direct(RenderArgs A, int64_t nv, const uint32_t* __restrict__ vflags,
@@ -601,13 +661,21 @@ hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light*
   {
     PhaseTimer tm(PH_PATHS, s);
     if (NG > 0) {
-      k_diffuse_rays<<<grid_for(NG, kRBlock), kRBlock, 0, s>>>(S, J->cq.p, J->gdir.p, NG, J->gvalid.p, J->gq.p,
-                                                               J->galb.p, sc->overflow.p);
+      if (PM_RAY_POOL)
+        k_diffuse_rays_pool<<<grid_for(NG, pool_chunk(NG, kRBlock)), kRBlock, 0, s>>>(
+            S, J->cq.p, J->gdir.p, NG, J->gvalid.p, J->gq.p, J->galb.p, sc->overflow.p, pool_chunk(NG, kRBlock));
+      else
+        k_diffuse_rays<<<grid_for(NG, kRBlock), kRBlock, 0, s>>>(S, J->cq.p, J->gdir.p, NG, J->gvalid.p, J->gq.p,
+                                                                 J->galb.p, sc->overflow.p);
       PM_HIP_TRY(hipGetLastError());
     }
     if (NS > 0) {
-      k_shadow_rays<<<grid_for(NS, kRBlock), kRBlock, 0, s>>>(S, J->cq.p, J->sray.p, nl, NS, J->svis.p,
-                                                              sc->overflow.p);
+      if (PM_RAY_POOL)
+        k_shadow_rays_pool<<<grid_for(NS, pool_chunk(NS, kRBlock)), kRBlock, 0, s>>>(
+            S, J->cq.p, J->sray.p, nl, NS, J->svis.p, sc->overflow.p, pool_chunk(NS, kRBlock));
+      else
+        k_shadow_rays<<<grid_for(NS, kRBlock), kRBlock, 0, s>>>(S, J->cq.p, J->sray.p, nl, NS, J->svis.p,
+                                                                sc->overflow.p);
       PM_HIP_TRY(hipGetLastError());
     }
     if (NV > 0) {

@@ -159,6 +159,29 @@ __global__ __launch_bounds__(kTBlock) void k_ph_trace(DevScene S, const PhotonRa
   hits[i] = make_float2(h.t, __int_as_float(h.slot));
 }
 
+// PM_RAY_POOL (build knob, default on): the bounce rays go through the chunked
+// ray pool (traverse_pool) instead of one ray per lane.
+#ifndef PM_RAY_POOL
+#define PM_RAY_POOL 1
+#endif
+__global__ __launch_bounds__(kTBlock) void k_ph_trace_pool(DevScene S, const PhotonRay* __restrict__ rays, int64_t n,
+                                                           float2* __restrict__ hits, int* overflow, int chunk) {
+  __shared__ int stack[kStackDepth * kTBlock];
+  __shared__ int lnext;
+  if (threadIdx.x == 0) lnext = 0;
+  __syncthreads();
+  traverse_pool<false>(
+      S, stack + threadIdx.x, kTBlock, overflow, n, chunk, &lnext,
+      [&](int64_t i, Ray& r, float& tmin, float& tmax) {
+        const float4 o = rays[i].o, d = rays[i].d;
+        ray_prep(r, v3{o.x, o.y, o.z}, v3{d.x, d.y, d.z});
+        tmin = kEPS;
+        tmax = kPhotonTmax;
+        return true;
+      },
+      [&](int64_t i, const Ray&, const HitInfo& h) { hits[i] = make_float2(h.t, __int_as_float(h.slot)); });
+}
+
 // Surviving rays are appended with ONE atomic per 1024-thread block (a
 // same-address atomic per wave serialised at one L2 channel: ~2/3 of the
 // kernel). With `keys`, the next bounce's sort key (top `mbits` of the origin's
@@ -305,7 +328,11 @@ hipError_t launch_trace_wavefront(pm_scene* sc, const LightDev* d_lights, const 
     const bool last = b + 1 >= maxd;
     const bool sort_next = sort_rays && !last;
     PM_HIP_TRY(hipMemsetAsync(counts.p, 0, sizeof(uint32_t), s));
-    k_ph_trace<<<grid_for(live, kTBlock), kTBlock, 0, s>>>(sc->view(), cur, live, hits.p, sc->overflow.p);
+    if (PM_RAY_POOL)
+      k_ph_trace_pool<<<grid_for(live, pool_chunk(live, kTBlock)), kTBlock, 0, s>>>(sc->view(), cur, live, hits.p,
+                                                                                    sc->overflow.p, pool_chunk(live, kTBlock));
+    else
+      k_ph_trace<<<grid_for(live, kTBlock), kTBlock, 0, s>>>(sc->view(), cur, live, hits.p, sc->overflow.p);
     PM_HIP_TRY(hipGetLastError());
     k_ph_shade<<<grid_for(live, kShadeBlock), kShadeBlock, 0, s>>>(sc->view(), cur, live, hits.p, nxt, counts.p, np,
                                                                    maxd, caustic, slots, cnt,
