@@ -5,4 +5,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -3 gpurun_out/gpu_tests.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 || { echo BENCH_FAILED; tail -20 gpurun_out/bench.log; exit 2; }
 tail -1 gpurun_out/bench.log
-bash profiles_run.sh r01b || exit 3
+bash profiles_run.sh ${1:-r01c} || exit 3

@@ -14,6 +14,7 @@ import collections
 import csv
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -51,16 +52,21 @@ def main(tag="r01", src=os.path.join(ROOT, "gpurun_out", "prof"), workload=None)
         out[k] = e
     with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
-    g = [k for k in out if "k_gather<1" in k]
+    # the global-map gather phase: k_gather<1,...> (modes 0-11, 14) or the seeded pair
+    # k_gather_lead<1,...> + k_gather_seeded<1,...> (modes 12/13, default): per-phase sums
+    g = [k for k in out if re.search(r"k_gather(_lead|_seeded)?<1,", k)]
     sha_file = os.path.join(src, "lib.sha256")
     lib_sha = open(sha_file).read().split()[0] if os.path.exists(sha_file) else None
     if g and workload is not None:
-        e = out[g[0]]
+        tot = lambda c: sum(out[k].get(c) or 0.0 for k in g) if all(c in out[k] for k in g) else None
+        fetch, write = tot("FETCH_SIZE"), tot("WRITE_SIZE")
         with open(os.path.join(dst, "pmc_gather_global.json"), "w") as f:
-            json.dump({"kernel": g[0], "workload": workload, "tag": tag, "lib_sha256": lib_sha,
-                       "fetch_kib": e.get("FETCH_SIZE"), "write_kib": e.get("WRITE_SIZE"),
-                       "hbm_bytes_per_launch": e.get("hbm_bytes_per_launch"),
-                       "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (calibrated for wide coalesced "
+            json.dump({"kernel": " + ".join(sorted(g)), "workload": workload, "tag": tag, "lib_sha256": lib_sha,
+                       "fetch_kib": fetch, "write_kib": write,
+                       "hbm_bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None
+                       else None,
+                       "note": "per global-gather phase (sum of its kernels, one launch each per frame); "
+                               "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (calibrated for wide coalesced "
                                "reads; this kernel gathers 16-B nodes, so the absolute is uncalibrated)"}, f,
                       indent=1)
     print(json.dumps({k[:60]: v.get("hbm_bytes_per_launch") for k, v in out.items()}, indent=1))
