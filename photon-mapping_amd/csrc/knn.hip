@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "pm_internal.hpp"
 
@@ -221,79 +222,111 @@ __device__ __forceinline__ float lean_cut(float r2) { return __uint_as_float(__f
 //    close-child ancestor-or-self (one step, one cached load), where the
 //    post-order point test and the far decision run. Same visited set, same
 //    point tests, fewer dependent loads.
+// Walk state of one lane (knn_walk_lean).
+struct LeanWalk {
+  float bound;
+  int prev, curr;
+  uint32_t far_mask;   // JUMP: bit d set <=> the path's depth-d node is a far child
+  int depth;           // JUMP: depth of curr
+  bool walking;
+  int qn;              // queued candidates in this lane's LDS column
+  __device__ __forceinline__ void start(float b, bool valid) {
+    bound = b;
+    prev = -1;
+    curr = 0;
+    far_mask = 0;
+    depth = 0;
+    walking = valid;
+  }
+};
+
+// One walk step of every lane (finished / idle lanes re-read their last node and
+// are masked): the post-order point test queues a candidate, the walk moves on.
+template <int K, bool JUMP>
+__device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, int n, v3 q, const double (&list)[K],
+                                          LeanWalk& w, double* lq, int lstride) {
+  const float4 nd = nodes[w.curr];
+  const int child = 2 * w.curr + 1;
+  const int wd = __float_as_int(nd.w);
+  const int dim = wd & 3;
+  const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
+  const float diff = dim == 0 ? dx : (dim == 1 ? dy : dz);   // = q[dim] - nd[dim]
+  const int side = diff > 0.f ? 1 : 0;
+  const int close_c = child + side, far_c = child + 1 - side;
+  const int parent = ((w.curr + 1) >> 1) - 1;
+  const bool down = w.prev < child;
+  const bool test = (down && close_c >= n) || w.prev == close_c;
+  const float d2 = dx * dx + dy * dy + dz * dz;
+  const double key = key_make(d2, (uint32_t)(wd >> 2));
+  const bool cand = w.walking && test && key < list[K - 1];
+  int next, nprev;
+  if (JUMP) {
+    if (down && close_c < n) {
+      next = close_c;
+      nprev = w.curr;
+      w.far_mask &= ~(2u << w.depth);
+      w.depth++;
+    } else if (far_c < n && diff * diff <= w.bound) {
+      next = far_c;
+      nprev = w.curr;
+      w.far_mask |= 2u << w.depth;
+      w.depth++;
+    } else {
+      // curr is finished: deepest close-child ancestor-or-self a (depth da);
+      // bit 0 (the root) is always clear, so da = 0 ends the walk
+      const uint32_t open = (~w.far_mask & ((2u << w.depth) - 1u)) | 1u;
+      const int da = 31 - __clz(open);
+      const int a = ((w.curr + 1) >> (w.depth - da)) - 1;
+      next = da == 0 ? -1 : ((a + 1) >> 1) - 1;
+      nprev = a;
+      w.depth = da - 1;
+    }
+  } else {
+    if (w.prev == far_c) next = parent;
+    else if (w.prev == close_c || close_c >= n) next = (far_c < n && diff * diff <= w.bound) ? far_c : parent;
+    else next = close_c;
+    nprev = w.curr;
+  }
+  lq[w.qn * lstride] = key;
+  w.qn += cand ? 1 : 0;
+  const bool go = w.walking && next >= 0;
+  w.prev = go ? nprev : w.prev;
+  w.curr = go ? next : w.curr;
+  w.walking = go;
+}
+
+// Wave-uniform insert round: every lane with a queued key pops one.
+template <int K>
+__device__ __forceinline__ void lean_round(double (&list)[K], LeanWalk& w, const double* lq, int lstride) {
+  const bool pop = w.qn > 0;
+  w.qn -= pop ? 1 : 0;
+  const double ik = pop ? lq[w.qn * lstride] : __longlong_as_double(0x7FEFFFFFFFFFFFFFll);
+  if (ik < list[K - 1]) {
+    list_insert<K>(list, ik);
+    w.bound = key_d2(list[K - 1]);
+  }
+}
+
+__device__ __forceinline__ double lean_sentinel(float cut) {
+  return __longlong_as_double((long long)((((uint64_t)__float_as_uint(cut)) << 32 | 0xFFFFFFFFull) + kKeyBias));
+}
+
 template <int K, int QL, bool JUMP = false>
 __device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float cut, bool valid,
                                               double (&list)[K], double* lq, int lstride) {
-  const double sentinel =
-      __longlong_as_double((long long)((((uint64_t)__float_as_uint(cut)) << 32 | 0xFFFFFFFFull) + kKeyBias));
+  const double sentinel = lean_sentinel(cut);
 #pragma unroll
   for (int j = 0; j < K; j++) list[j] = sentinel;
   if (n <= 0) return;   // empty map: every lane keeps the sentinel list (uniform)
-  float bound = key_d2(sentinel);
-  int prev = -1, curr = 0;
-  uint32_t far_mask = 0;   // JUMP: bit d set <=> the path's depth-d node is a far child
-  int depth = 0;           // JUMP: depth of curr
-  bool walking = valid;
-  int qn = 0;
+  LeanWalk w;
+  w.start(key_d2(sentinel), valid);
+  w.qn = 0;
   for (;;) {
-    const float4 nd = nodes[curr];   // finished / invalid lanes re-read a valid node
-    const int child = 2 * curr + 1;
-    const int w = __float_as_int(nd.w);
-    const int dim = w & 3;
-    const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
-    const float diff = dim == 0 ? dx : (dim == 1 ? dy : dz);   // = q[dim] - nd[dim]
-    const int side = diff > 0.f ? 1 : 0;
-    const int close_c = child + side, far_c = child + 1 - side;
-    const int parent = ((curr + 1) >> 1) - 1;
-    const bool down = prev < child;
-    const bool test = (down && close_c >= n) || prev == close_c;
-    const float d2 = dx * dx + dy * dy + dz * dz;
-    const double key = key_make(d2, (uint32_t)(w >> 2));
-    const bool cand = walking && test && key < list[K - 1];
-    int next, nprev;
-    if (JUMP) {
-      if (down && close_c < n) {
-        next = close_c;
-        nprev = curr;
-        far_mask &= ~(2u << depth);
-        depth++;
-      } else if (far_c < n && diff * diff <= bound) {
-        next = far_c;
-        nprev = curr;
-        far_mask |= 2u << depth;
-        depth++;
-      } else {
-        // curr is finished: deepest close-child ancestor-or-self a (depth da);
-        // bit 0 (the root) is always clear, so da = 0 ends the walk
-        const uint32_t open = (~far_mask & ((2u << depth) - 1u)) | 1u;
-        const int da = 31 - __clz(open);
-        const int a = ((curr + 1) >> (depth - da)) - 1;
-        next = da == 0 ? -1 : ((a + 1) >> 1) - 1;
-        nprev = a;
-        depth = da - 1;
-      }
-    } else {
-      if (prev == far_c) next = parent;
-      else if (prev == close_c || close_c >= n) next = (far_c < n && diff * diff <= bound) ? far_c : parent;
-      else next = close_c;
-      nprev = curr;
-    }
-    lq[qn * lstride] = key;
-    qn += cand ? 1 : 0;
-    const bool go = walking && next >= 0;
-    prev = go ? nprev : prev;
-    curr = go ? next : curr;
-    walking = go;
-    const bool any_walking = __ballot(walking) != 0;
-    if (__ballot(qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
-      const bool pop = qn > 0;
-      qn -= pop ? 1 : 0;
-      const double ik = pop ? lq[qn * lstride] : __longlong_as_double(0x7FEFFFFFFFFFFFFFll);
-      if (ik < list[K - 1]) {
-        list_insert<K>(list, ik);
-        bound = key_d2(list[K - 1]);
-      }
-      if (!any_walking && __ballot(qn > 0) == 0) break;
+    lean_step<K, JUMP>(nodes, n, q, list, w, lq, lstride);
+    const bool any_walking = __ballot(w.walking) != 0;
+    if (__ballot(w.qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
+      lean_round<K>(list, w, lq, lstride);
+      if (!any_walking && __ballot(w.qn > 0) == 0) break;
     }
   }
 }
@@ -378,8 +411,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 // Seeded cut-off (PM_GATHER_MODE 12; 13 = with the JUMP walk, default). Every kSeedStride-th query
-// in walk order is a LEADER; k_gather_lead runs the leaders with the plain
-// cut-off and keeps (position, K-th d^2). The other queries then start from a
+// in walk order is a LEADER; the first k_gather_level launch runs the leaders
+// with the plain cut-off and keeps (position, K-th d^2). The other queries then start from a
 // cut-off that provably holds the K nearest: the leader's K points lie within
 // sqrt(t') of q', hence within sqrt(t') + |q - q'| of q (triangle inequality),
 // so at least K photons have d^2 <= that bound and the K smallest keys -- the
@@ -393,7 +426,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 // leaders 50.9, 8/4 50.3, 4/2 52.2, 16/2 50.6, 16/4 49.8. A follower bound from
 // the union of the enclosing leaders' neighbour sets (K-th smallest distance,
 // exact by construction) was tighter but slower: 54.6 (its 1.6 KB of leader
-// points per follower cost more than the walk saved).
+// points per follower cost more than the walk saved). Seed tightness on config 3
+// (PM_GATHER_SEEDSTATS): even the previous query in walk order gives a mean
+// bound / exact K-th d^2 of 2.8 on the global map, the stride-8 pair 2.8; the
+// exact-cut re-walk (mode 16) takes 34.4 ms, the floor of any seeding. Leader
+// hierarchies (PM_SEED_LEVELS) measured slower: 256,16 52.7; 16,8 51.6;
+// 16,4 52.0; 4096,256,16 54.5. A pooled variant (lanes refill from a per-
+// workgroup chunk, as in traverse_pool) ran 2.5x slower: the 100-VGPR list plus
+// the walk state leave no room for the pool's state (30 VGPRs spilled at 128).
 #ifndef PM_SEED_STRIDE
 #define PM_SEED_STRIDE 16
 #endif
@@ -417,60 +457,55 @@ __device__ __forceinline__ float seed_cut(double bound, float r2) {
   return fminf(f, plain);
 }
 
-// leaders: lane j takes walk rank j * kSeedStride (query perm[rank])
-template <int TAG, int QL, bool JUMP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_lead(
-    const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
-    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
-    int64_t nlead) {
-  __shared__ double lq[QL * 256];
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = j < nlead;
-  const int64_t r = j * kSeedStride;
-  const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
-  const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  double list[kKNearest];
-  const float R2 = kKMaxDistance * kKMaxDistance;
-  knn_walk_lean<kKNearest, QL, JUMP>(nodes, n, v3{qq.x, qq.y, qq.z}, lean_cut(R2), valid, list, lq + threadIdx.x,
-                                     256);
-  if (valid) {
-    const bool full = key_id(list[kKNearest - 1]) != 0xFFFFFFFFu;
-    const v3 f = radiance(list, payload, qq.w, full ? key_d2(list[kKNearest - 1]) : R2);
-    out[i] = make_float4(f.x, f.y, f.z, 0.f);
-    lead[j] = make_float4(qq.x, qq.y, qq.z, full ? key_d2(list[kKNearest - 1]) : -1.f);
+// One level of the seeded gather (modes 12 / 13). Walk ranks of this level: the
+// multiples of `stride` that are not multiples of `sstride` (sstride = 0: every
+// multiple, the top level, plain cut-off). Its cut-off comes from the records of
+// the enclosing level (ranks that are multiples of sstride: the enclosing pair plus
+// one more on each side). A level with stride >= gran (the finest leader stride)
+// records (position, K-th d^2) of its queries in lead[rank / gran]. Levels
+// "256,16" (PM_SEED_LEVELS): the stride-16 leaders no longer walk with the plain
+// cut-off (2.6x a follower's cost per query) but are seeded by stride-256 ones.
+// walk rank of the t-th query of a level (see k_gather_level)
+__device__ __forceinline__ int64_t level_rank(int64_t t, int64_t stride, int64_t sstride) {
+  if (sstride == 0) return t * stride;
+  const int64_t m = sstride / stride;
+  return ((t / (m - 1)) * m + 1 + t % (m - 1)) * stride;
+}
+// cut-off of rank r from the enclosing level's records
+__device__ __forceinline__ float level_cut(const float4* __restrict__ lead, int64_t nq, int64_t r, int64_t sstride,
+                                           int64_t gran, v3 q, float R2) {
+  if (sstride <= 0) return lean_cut(R2);
+  const int64_t jp = r / sstride, ls = sstride / gran, ns = (nq - 1) / sstride + 1;
+  double b = seed_bound(lead[jp * ls], q);
+  if (jp + 1 < ns) b = fmin(b, seed_bound(lead[(jp + 1) * ls], q));
+  if (PM_SEED_LEADERS > 2) {
+    if (jp >= 1) b = fmin(b, seed_bound(lead[(jp - 1) * ls], q));
+    if (jp + 2 < ns) b = fmin(b, seed_bound(lead[(jp + 2) * ls], q));
   }
+  return seed_cut(b, R2);
 }
 
-// followers: lane t takes the t-th non-leader walk rank
 template <int TAG, int QL, bool JUMP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_seeded(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
-    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, const float4* __restrict__ lead,
-    int64_t nlead) {
+    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
+    int64_t stride, int64_t sstride, int64_t gran) {
   __shared__ double lq[QL * 256];
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t r = (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
+  const int64_t r = level_rank(t, stride, sstride);
   const bool valid = r < nq;
   const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   const v3 q = {qq.x, qq.y, qq.z};
   const float R2 = kKMaxDistance * kKMaxDistance;
-  float cut = lean_cut(R2);
-  if (valid) {
-    const int64_t jp = r / kSeedStride;
-    double b = seed_bound(lead[jp], q);
-    if (jp + 1 < nlead) b = fmin(b, seed_bound(lead[jp + 1], q));
-    if (PM_SEED_LEADERS > 2) {
-      if (jp >= 1) b = fmin(b, seed_bound(lead[jp - 1], q));
-      if (jp + 2 < nlead) b = fmin(b, seed_bound(lead[jp + 2], q));
-    }
-    cut = seed_cut(b, R2);
-  }
+  const float cut = valid ? level_cut(lead, nq, r, sstride, gran, q, R2) : lean_cut(R2);
   double list[kKNearest];
   knn_walk_lean<kKNearest, QL, JUMP>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
   if (valid) {
-    const v3 f = radiance(list, payload, qq.w, radiance_r2(list, R2));
+    const bool full = key_id(list[kKNearest - 1]) != 0xFFFFFFFFu;
+    const v3 f = radiance(list, payload, qq.w, full ? key_d2(list[kKNearest - 1]) : R2);
     out[i] = make_float4(f.x, f.y, f.z, 0.f);
+    if (stride >= gran) lead[r / gran] = make_float4(qq.x, qq.y, qq.z, full ? key_d2(list[kKNearest - 1]) : -1.f);
   }
 }
 
@@ -626,6 +661,26 @@ __global__ void k_unpack_out(const float4* o, int64_t nq, pm_float3* out) {
   out[i] = {o[i].x, o[i].y, o[i].z};
 }
 
+// Leader strides of the seeded gather, coarsest first, each a multiple of the
+// next (PM_SEED_LEVELS, e.g. "256,16"; read per launch). Default: PM_SEED_STRIDE alone.
+static std::vector<int64_t> seed_levels() {
+  std::vector<int64_t> v;
+  {
+    const char* e = std::getenv("PM_SEED_LEVELS");
+    if (e) {
+      for (const char* p = e; *p;) {
+        char* q = nullptr;
+        const long long x = std::strtoll(p, &q, 10);
+        if (q == p) break;
+        if (x >= 2 && (v.empty() || (v.back() % x == 0 && v.back() > x))) v.push_back(x);
+        p = (*q == ',') ? q + 1 : q;
+      }
+    }
+    if (v.empty()) v.push_back(kSeedStride);
+  }
+  return v;
+}
+
 hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int k, float radius, int32_t* ids,
                       float* d2, float* maxd2, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
@@ -659,10 +714,10 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
                          int tag, const uint32_t* perm) {
   if (nq <= 0) return hipSuccess;
   // A/B knob (read per launch), all variants return identical bits:
-  //  13 (default) mode 12 with the JUMP walk                   50.9 ms
+  //  13 (default) mode 12 with the JUMP walk                   49.8 ms
   //  14 mode 11 with the JUMP walk                             59.0 ms
   //  16 / 17 diagnostic: exact-cut re-walk (JUMP / plain), see k_gather_exactcut
-  //  12 mode 11 behind leader-seeded cut-offs (k_gather_lead / _seeded)   53.5 ms
+  //  12 mode 11 behind leader-seeded cut-offs (k_gather_level)   53.5 ms
   //  11 mode 9 with the lean step (knn_walk_lean)   62.3 ms
   //   9 post-order + 8-deep LDS insert queue                  66.7 ms
   //   4 post-order, insert at once                             73.6 ms
@@ -676,20 +731,30 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   if (std::getenv("PM_GATHER_SEEDSTATS")) seed_stats(m, qb, nq, s, perm);
   const int g = grid_for(nq, 256);
   const int n = (int)m->n;
-  if ((mode == 12 || mode == 13) && nq > kSeedStride) {
-    const int64_t nlead = (nq + kSeedStride - 1) / kSeedStride;
-    DevBuf<float4> lead(nlead);
+  const std::vector<int64_t> lv = seed_levels();
+  if ((mode == 12 || mode == 13) && nq > lv.back()) {
+    const int64_t gran = lv.back();
+    DevBuf<float4> lead((nq + gran - 1) / gran);
     if (!lead.p) return hipErrorOutOfMemory;
-    const int gl = grid_for(nlead, 256), gf = grid_for(nq - nlead, 256);
-#define PM_SEEDED(T, J)                                                                                     \
-  k_gather_lead<T, 8, J><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead); \
-  k_gather_seeded<T, 8, J><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, nlead);
-    if (tag == 1 && mode == 13) { PM_SEEDED(1, true) }
-    else if (tag == 1) { PM_SEEDED(1, false) }
-    else if (mode == 13) { PM_SEEDED(0, true) }
-    else { PM_SEEDED(0, false) }
-#undef PM_SEEDED
-    return hipGetLastError();
+    int64_t sstride = 0;
+    for (size_t l = 0; l <= lv.size(); l++) {
+      const int64_t stride = l < lv.size() ? lv[l] : 1;
+      const int64_t nr = (nq + stride - 1) / stride - (sstride ? (nq + sstride - 1) / sstride : 0);
+      {
+        const int gl = grid_for(nr, 256);
+#define PM_LEVEL(T, J)                                                                                         \
+  k_gather_level<T, 8, J><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, stride, \
+                                             sstride, gran)
+        if (tag == 1 && mode == 13) PM_LEVEL(1, true);
+        else if (tag == 1) PM_LEVEL(1, false);
+        else if (mode == 13) PM_LEVEL(0, true);
+        else PM_LEVEL(0, false);
+#undef PM_LEVEL
+      }
+      PM_HIP_TRY(hipGetLastError());
+      sstride = stride;
+    }
+    return hipSuccess;
   }
   if (mode == 16 || mode == 17) {
     DevBuf<float> cutb(nq);

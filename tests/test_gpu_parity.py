@@ -483,11 +483,13 @@ def test_render_continuation_rerun(sphere, monkeypatch):
     assert np.array_equal(_bits(ra.cpu().numpy()), _bits(rb.cpu().numpy()))
 
 
+@pytest.mark.parametrize("levels", [None, "256,16", "64,8,2"])
 @pytest.mark.parametrize("jitter", [0.0, 1e-3, 0.5])
-def test_seeded_gather_tight_neighbours(cornell, monkeypatch, jitter):
+def test_seeded_gather_tight_neighbours(cornell, monkeypatch, jitter, levels):
     """Mode 12 (leader-seeded cut-offs) on queries in spatial order, where the
     leader bounds are tight: queries at photon positions (d^2 = 0 ties),
-    duplicated queries and small jitters. Bitwise equal to the plain walk."""
+    duplicated queries and small jitters; one seed level (default) and leader
+    levels seeded by coarser leaders (PM_SEED_LEVELS),. Bitwise equal to the plain walk."""
     import pm_amd
     meshes, lights = cornell
     gs = pm_amd.Scene(meshes)
@@ -504,6 +506,8 @@ def test_seeded_gather_tight_neighbours(cornell, monkeypatch, jitter):
     brdf = torch.from_numpy(rng.uniform(0, 0.4, size=len(q)).astype(np.float32)).cuda()
     monkeypatch.setenv("PM_GATHER_MODE", "11")
     ref = [pm_amd.gather_photons(m, qt, brdf).cpu().numpy() for m in (gm, cm)]
+    if levels:
+        monkeypatch.setenv("PM_SEED_LEVELS", levels)
     for mode in ("12", "13", "14"):
         monkeypatch.setenv("PM_GATHER_MODE", mode)
         for m, r in zip((gm, cm), ref):

@@ -53,8 +53,8 @@ def main(tag="r01", src=os.path.join(ROOT, "gpurun_out", "prof"), workload=None)
     with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     # the global-map gather phase: k_gather<1,...> (modes 0-11, 14) or the seeded pair
-    # k_gather_lead<1,...> + k_gather_seeded<1,...> (modes 12/13, default): per-phase sums
-    g = [k for k in out if re.search(r"k_gather(_lead|_seeded)?<1,", k)]
+    # k_gather_level<1,...> launches (modes 12/13, default): per-phase sums
+    g = [k for k in out if re.search(r"k_gather(_lead|_seeded|_level)?<1,", k)]
     sha_file = os.path.join(src, "lib.sha256")
     lib_sha = open(sha_file).read().split()[0] if os.path.exists(sha_file) else None
     if g and workload is not None:
