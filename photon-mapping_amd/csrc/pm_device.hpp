@@ -258,6 +258,25 @@ __device__ __forceinline__ bool slab(float x0, float x1, float y0, float y1, flo
   return tn <= tf;
 }
 
+// Slab test on (x0, x1, ...) with the origin term folded into one fma per plane:
+// t = fma(x, inv, -o * inv) (noi = -o * inv, once per node). Culling only: the
+// boxes are padded by 1e-5 x the scene extent and the limit by 1.00001 (see
+// build_lbvh), far above the one-rounding difference to (x - o) * inv, so the
+// triangles tested -- and the argmin result -- are unchanged. PM_SLAB_FMA = 0
+// keeps the two-op form (A/B build knob).
+#ifndef PM_SLAB_FMA
+#define PM_SLAB_FMA 1
+#endif
+__device__ __forceinline__ bool slab_fma(float x0, float x1, float y0, float y1, float z0, float z1, const Ray& r,
+                                         v3 noi, float tmin, float tmax, float& tn) {
+  const float t0x = __builtin_fmaf(x0, r.inv.x, noi.x), t1x = __builtin_fmaf(x1, r.inv.x, noi.x);
+  const float t0y = __builtin_fmaf(y0, r.inv.y, noi.y), t1y = __builtin_fmaf(y1, r.inv.y, noi.y);
+  const float t0z = __builtin_fmaf(z0, r.inv.z, noi.z), t1z = __builtin_fmaf(z1, r.inv.z, noi.z);
+  tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+  const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
+  return tn <= tf;
+}
+
 // Traversal stack: the top kStackDepth entries live in LDS ([depth][blockDim],
 // sized for occupancy: 16 x 4 B x 64 lanes = 4 KB per wave); deeper entries
 // spill to a per-lane private (scratch) array that only deep paths touch.
@@ -372,10 +391,19 @@ __device__ __forceinline__ bool traverse_step(const DevScene& S, const Ray& r, f
   const int4 ch = *reinterpret_cast<const int4*>(&q[6]);
   const float lim = (ANY || h.slot < 0) ? tmax * 1.00001f : h.t * 1.00001f;
   float t0, t1, t2, t3;
-  const bool b0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, tmin, lim, t0) && ch.x != kBvhEmpty;
-  const bool b1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tmin, lim, t1) && ch.y != kBvhEmpty;
-  const bool b2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tmin, lim, t2) && ch.z != kBvhEmpty;
-  const bool b3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tmin, lim, t3) && ch.w != kBvhEmpty;
+  bool b0, b1, b2, b3;
+  if (PM_SLAB_FMA) {
+    const v3 noi = {-r.o.x * r.inv.x, -r.o.y * r.inv.y, -r.o.z * r.inv.z};
+    b0 = slab_fma(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, noi, tmin, lim, t0) && ch.x != kBvhEmpty;
+    b1 = slab_fma(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, noi, tmin, lim, t1) && ch.y != kBvhEmpty;
+    b2 = slab_fma(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, noi, tmin, lim, t2) && ch.z != kBvhEmpty;
+    b3 = slab_fma(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, noi, tmin, lim, t3) && ch.w != kBvhEmpty;
+  } else {
+    b0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, tmin, lim, t0) && ch.x != kBvhEmpty;
+    b1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tmin, lim, t1) && ch.y != kBvhEmpty;
+    b2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tmin, lim, t2) && ch.z != kBvhEmpty;
+    b3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tmin, lim, t3) && ch.w != kBvhEmpty;
+  }
   // leaves first: a hit shrinks the limit applied to the internal children
   if (PM_LEAF_BATCH == 4) {
     const bool lv[4] = {b0 && ch.x < 0, b1 && ch.y < 0, b2 && ch.z < 0, b3 && ch.w < 0};
