@@ -370,7 +370,140 @@ __global__ void k_collapse_link(const int2* __restrict__ frontier, int nf, const
   *cp = c;
 }
 
-static hipError_t collapse_bvh4(const float4* bin, int nbin, pm_scene* sc, hipStream_t s) {
+// ---------------------------------------------------------------- BVH8 (quantised)
+// PM_BVH_WIDTH 8: the same greedy collapse opens 6 times (8 children) and the
+// node stores its children's boxes as 8-bit offsets from the node's corner p in
+// units of a per-axis power of two s (128 B, one cache line):
+//   f4[0]    p.xyz, exponent bytes (IEEE biased) of s.x | s.y << 8 | s.z << 16
+//   f4[1..2] child codes [8] (>= 0 node, kBvhEmpty unused, else ~triangle slot)
+//   f4[3..5] per axis: qlo[8] bytes (2 dwords), qhi[8] bytes (2 dwords)
+// The decoded box p + q * s (q * s exact, one rounding) CONTAINS the padded child
+// box: each q is stepped outwards until the float decode does, so culling stays
+// conservative and the traversal's argmin result is unchanged.
+__device__ __forceinline__ float q_decode(float p, uint32_t q, float sc) { return p + (float)q * sc; }
+
+__global__ void k_collapse_open8(const float4* __restrict__ bin, const int2* __restrict__ frontier, int nf,
+                                 float4* __restrict__ q, uint32_t* __restrict__ cnt) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nf) return;
+  const int2 fr = frontier[f];
+  int code[8];
+  float box[8][6];
+  const float* nb = reinterpret_cast<const float*>(&bin[4 * fr.x]);
+  const int4 c2 = *reinterpret_cast<const int4*>(&bin[4 * fr.x + 3]);
+  code[0] = c2.x;
+  code[1] = c2.y;
+#pragma unroll
+  for (int k = 0; k < 6; k++) box[0][k] = nb[k], box[1][k] = nb[6 + k];
+  int m = 2;
+  for (int it = 0; it < 6; it++) {
+    int best = -1;
+    float barea = -1.0f;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      if (c < m && code[c] >= 0) {
+        const float a = box_area(box[c]);
+        if (a > barea) barea = a, best = c;
+      }
+    }
+    if (best < 0) break;
+    const float* ob = reinterpret_cast<const float*>(&bin[4 * code[best]]);
+    const int4 oc = *reinterpret_cast<const int4*>(&bin[4 * code[best] + 3]);
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      if (c == best) {
+        code[c] = oc.x;
+#pragma unroll
+        for (int k = 0; k < 6; k++) box[c][k] = ob[k];
+      } else if (c == m) {
+        code[c] = oc.y;
+#pragma unroll
+        for (int k = 0; k < 6; k++) box[c][k] = ob[6 + k];
+      }
+    }
+    m++;
+  }
+  // node corner and per-axis scale
+  float p[3], hi[3];
+  uint32_t eb[3];
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    p[a] = box[0][2 * a];
+    hi[a] = box[0][2 * a + 1];
+#pragma unroll
+    for (int c = 1; c < 8; c++) {
+      if (c < m) {
+        p[a] = fminf(p[a], box[c][2 * a]);
+        hi[a] = fmaxf(hi[a], box[c][2 * a + 1]);
+      }
+    }
+    const double ext = (double)hi[a] - (double)p[a];
+    int e = 1;   // biased exponent of s
+    if (ext > 0.0) {
+      int k;
+      frexp(ext / 255.0, &k);   // ext / 255 < 2^k
+      e = k + 127;
+    }
+    e = e < 1 ? 1 : e;
+    while (e < 254 && q_decode(p[a], 255u, __uint_as_float((uint32_t)e << 23)) < hi[a]) e++;
+    eb[a] = (uint32_t)e;
+  }
+  uint32_t qw[3][4] = {};   // per axis: qlo dwords 0,1; qhi dwords 2,3
+  uint32_t internal = 0;
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    const bool used = c < m;
+    if (used && code[c] >= 0) internal++;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      uint32_t ql = 0, qh = 0;
+      if (used) {
+        const float sc = __uint_as_float(eb[a] << 23);
+        const double inv = 1.0 / (double)sc;
+        double dl = floor(((double)box[c][2 * a] - (double)p[a]) * inv);
+        double dh = ceil(((double)box[c][2 * a + 1] - (double)p[a]) * inv);
+        ql = (uint32_t)fmin(fmax(dl, 0.0), 255.0);
+        qh = (uint32_t)fmin(fmax(dh, 0.0), 255.0);
+        while (ql > 0 && q_decode(p[a], ql, sc) > box[c][2 * a]) ql--;
+        while (qh < 255 && q_decode(p[a], qh, sc) < box[c][2 * a + 1]) qh++;
+      }
+      qw[a][c >> 2] |= ql << (8 * (c & 3));
+      qw[a][2 + (c >> 2)] |= qh << (8 * (c & 3));
+    }
+  }
+  float4* qn = &q[8 * (int64_t)fr.y];
+  qn[0] = make_float4(p[0], p[1], p[2], __uint_as_float(eb[0] | eb[1] << 8 | eb[2] << 16));
+  int* cc = reinterpret_cast<int*>(&qn[1]);
+#pragma unroll
+  for (int c = 0; c < 8; c++) cc[c] = c < m ? code[c] : kBvhEmpty;   // patched by k_collapse_link8
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+    qn[3 + a] = make_float4(__uint_as_float(qw[a][0]), __uint_as_float(qw[a][1]), __uint_as_float(qw[a][2]),
+                            __uint_as_float(qw[a][3]));
+  qn[6] = make_float4(0.f, 0.f, 0.f, 0.f);
+  qn[7] = make_float4(0.f, 0.f, 0.f, 0.f);
+  cnt[f] = internal;
+}
+
+__global__ void k_collapse_link8(const int2* __restrict__ frontier, int nf, const uint32_t* __restrict__ off,
+                                 int base, float4* __restrict__ q, int2* __restrict__ next) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nf) return;
+  const int2 fr = frontier[f];
+  int* cc = reinterpret_cast<int*>(&q[8 * (int64_t)fr.y + 1]);
+  int o = (int)off[f];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int c = cc[k];
+    if (c >= 0) {
+      next[o] = make_int2(c, base + o);
+      cc[k] = base + o;
+      o++;
+    }
+  }
+}
+
+static hipError_t collapse_bvh(const float4* bin, int nbin, pm_scene* sc, hipStream_t s) {
   sc->nodes.alloc((size_t)8 * nbin);
   DevBuf<int2> fa(nbin), fb(nbin);
   DevBuf<uint32_t> cnt(nbin), off(nbin), total(1);
@@ -381,10 +514,12 @@ static hipError_t collapse_bvh4(const float4* bin, int nbin, pm_scene* sc, hipSt
   int2 *cur = fa.p, *nxt = fb.p;
   while (nf > 0) {
     depth++;
-    k_collapse_open<<<grid_for(nf, 256), 256, 0, s>>>(bin, cur, nf, sc->nodes.p, cnt.p);
+    if (kBvhWidth == 8) k_collapse_open8<<<grid_for(nf, 256), 256, 0, s>>>(bin, cur, nf, sc->nodes.p, cnt.p);
+    else k_collapse_open<<<grid_for(nf, 256), 256, 0, s>>>(bin, cur, nf, sc->nodes.p, cnt.p);
     PM_HIP_TRY(hipGetLastError());
     PM_HIP_TRY(exclusive_scan_u32(cnt.p, off.p, nf, total.p, s));
-    k_collapse_link<<<grid_for(nf, 256), 256, 0, s>>>(cur, nf, off.p, alloc, sc->nodes.p, nxt);
+    if (kBvhWidth == 8) k_collapse_link8<<<grid_for(nf, 256), 256, 0, s>>>(cur, nf, off.p, alloc, sc->nodes.p, nxt);
+    else k_collapse_link<<<grid_for(nf, 256), 256, 0, s>>>(cur, nf, off.p, alloc, sc->nodes.p, nxt);
     PM_HIP_TRY(hipGetLastError());
     uint32_t t = 0;
     PM_HIP_TRY(hipMemcpyAsync(&t, total.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -444,7 +579,7 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s
     const int ch[4] = {~0, ~0, 0, 0};
     std::memcpy(&node[12], ch, 16);
     PM_HIP_TRY(hipMemcpyAsync(bin.p, node, 64, hipMemcpyHostToDevice, s));
-    return collapse_bvh4(bin.p, nn, sc, s);
+    return collapse_bvh(bin.p, nn, sc, s);
   }
   DevBuf<uint32_t> codes(n), order(n);
   DevBuf<int4> child(nn);
@@ -463,7 +598,7 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s
   const char* benv = std::getenv("PM_BVH");
   if (!(benv && std::strcmp(benv, "lbvh") == 0)) {
     PM_HIP_TRY(build_ploc(sc->tri.p, n, pad, bin.p, s));
-    return collapse_bvh4(bin.p, nn, sc, s);
+    return collapse_bvh(bin.p, nn, sc, s);
   }
   PM_HIP_TRY(hipMemsetAsync(pint.p, 0, sizeof(int) * nn, s));
   k_hierarchy<<<grid_for(n - 1, 256), 256, 0, s>>>(codes.p, n, child.p, pint.p, pleaf.p);
@@ -473,7 +608,7 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s
   PM_HIP_TRY(hipGetLastError());
   k_pack_children<<<grid_for(nn, 256), 256, 0, s>>>(bin.p, child.p, nn);
   PM_HIP_TRY(hipGetLastError());
-  return collapse_bvh4(bin.p, nn, sc, s);
+  return collapse_bvh(bin.p, nn, sc, s);
 }
 
 // ---------------------------------------------------------------- queries

@@ -298,10 +298,22 @@ constexpr int kStackDepth = PM_STACK_DEPTH;
 #define PM_WAVES_ATTR(w) __attribute__((amdgpu_waves_per_eu((w) > 0 ? (w) : 1, (w) > 0 ? (w) : 10)))
 // PM_NO_SPILL: LDS stack only (no private scratch in any traversal kernel);
 // rays deeper than kStackDepth report PM_ERR_OVERFLOW. A/B and diagnostics.
+// BVH width (build knob, library-wide): 4 = 128-B float boxes, 8 = 128-B
+// quantised boxes (bvh.hip, k_collapse_open8). Width 8 passes the GPU suite
+// bitwise but measured slower on config 3: trace 33.3 -> 44.3 ms, paths 18.5 ->
+// 26.5 ms (79 VGPRs, 6 waves/SIMD; forced to 8 waves: 45.8 / 27.4 ms). A width-W BVH of depth D needs at
+// most (W - 1)(D - 1) stack entries: 64 in total for W = 4 (D <= 22), 128 for
+// W = 8 (D <= 19).
+#ifndef PM_BVH_WIDTH
+#define PM_BVH_WIDTH 4
+#endif
+constexpr int kBvhWidth = PM_BVH_WIDTH;
+static_assert(kBvhWidth == 4 || kBvhWidth == 8, "PM_BVH_WIDTH is 4 or 8");
+constexpr int kStackTotal = kBvhWidth == 8 ? 128 : 64;
 #ifdef PM_NO_SPILL
 constexpr int kSpillDepth = 0;
 #else
-constexpr int kSpillDepth = 64 - PM_STACK_DEPTH > 0 ? 64 - PM_STACK_DEPTH : 1;
+constexpr int kSpillDepth = kStackTotal - PM_STACK_DEPTH > 0 ? kStackTotal - PM_STACK_DEPTH : 1;
 #endif
 constexpr int32_t kBvhEmpty = INT32_MIN;
 
@@ -383,9 +395,9 @@ __device__ __forceinline__ bool leaf_batch(const DevScene& S, const Ray& r, floa
 // children, push the internal hits near-to-far and continue with the nearest,
 // or pop). Returns true when the ray is finished (stack empty, or an any-hit).
 template <bool ANY>
-__device__ __forceinline__ bool traverse_step(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
-                                              int stride, int* spill, int& node, int& sp, HitInfo& h,
-                                              int* overflow) {
+__device__ __forceinline__ bool traverse_step4(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
+                                               int stride, int* spill, int& node, int& sp, HitInfo& h,
+                                               int* overflow) {
   const float4* q = S.nodes + 8 * (int64_t)node;
   const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
   const int4 ch = *reinterpret_cast<const int4*>(&q[6]);
@@ -473,6 +485,116 @@ __device__ __forceinline__ bool traverse_step(const DevScene& S, const Ray& r, f
   sp--;
   node = (kSpillDepth == 0 || sp < kStackDepth) ? stack[sp * stride] : spill[sp - kStackDepth];
   return false;
+}
+
+// compare-and-swap on (t, code) pairs, ascending t
+__device__ __forceinline__ void cas8(float (&k)[8], int (&c)[8], int i, int j) {
+  const bool sw = k[j] < k[i];
+  const float ti = sw ? k[j] : k[i], tj = sw ? k[i] : k[j];
+  const int ci = sw ? c[j] : c[i], cj = sw ? c[i] : c[j];
+  k[i] = ti, k[j] = tj, c[i] = ci, c[j] = cj;
+}
+
+// BVH8 step (quantised node, see k_collapse_open8): decode the 8 child boxes in
+// ray-t space (t = q * (s * inv) + (p - o) * inv, one fma per plane; the boxes
+// are padded, so this culling is conservative like slab_fma), test the hit
+// leaves in compacted rounds, push the internal hits near-to-far (19-comparator
+// network) and continue with the nearest, or pop.
+template <bool ANY>
+__device__ __forceinline__ bool traverse_step8(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
+                                               int stride, int* spill, int& node, int& sp, HitInfo& h,
+                                               int* overflow) {
+  const float4* qn = S.nodes + 8 * (int64_t)node;
+  const float4 h0 = qn[0];
+  const int4 ca = *reinterpret_cast<const int4*>(&qn[1]);
+  const int4 cb = *reinterpret_cast<const int4*>(&qn[2]);
+  const uint4 qx = *reinterpret_cast<const uint4*>(&qn[3]);
+  const uint4 qy = *reinterpret_cast<const uint4*>(&qn[4]);
+  const uint4 qz = *reinterpret_cast<const uint4*>(&qn[5]);
+  const uint32_t eb = __float_as_uint(h0.w);
+  const float ax = __uint_as_float((eb & 0xFFu) << 23) * r.inv.x;
+  const float ay = __uint_as_float(((eb >> 8) & 0xFFu) << 23) * r.inv.y;
+  const float az = __uint_as_float(((eb >> 16) & 0xFFu) << 23) * r.inv.z;
+  const float bx = (h0.x - r.o.x) * r.inv.x, by = (h0.y - r.o.y) * r.inv.y, bz = (h0.z - r.o.z) * r.inv.z;
+  const float lim = (ANY || h.slot < 0) ? tmax * 1.00001f : h.t * 1.00001f;
+  int code[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
+  float tn[8];
+  uint32_t hitm = 0, leafm = 0;
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    const int sh = 8 * (c & 3);
+    const float lx = (float)(((c < 4 ? qx.x : qx.y) >> sh) & 0xFFu), hx = (float)(((c < 4 ? qx.z : qx.w) >> sh) & 0xFFu);
+    const float ly = (float)(((c < 4 ? qy.x : qy.y) >> sh) & 0xFFu), hy = (float)(((c < 4 ? qy.z : qy.w) >> sh) & 0xFFu);
+    const float lz = (float)(((c < 4 ? qz.x : qz.y) >> sh) & 0xFFu), hz = (float)(((c < 4 ? qz.z : qz.w) >> sh) & 0xFFu);
+    const float t0x = __builtin_fmaf(lx, ax, bx), t1x = __builtin_fmaf(hx, ax, bx);
+    const float t0y = __builtin_fmaf(ly, ay, by), t1y = __builtin_fmaf(hy, ay, by);
+    const float t0z = __builtin_fmaf(lz, az, bz), t1z = __builtin_fmaf(hz, az, bz);
+    tn[c] = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), lim));
+    const bool b = tn[c] <= tf && code[c] != kBvhEmpty;
+    hitm |= b ? (1u << c) : 0u;
+    leafm |= (b && code[c] < 0) ? (1u << c) : 0u;
+  }
+  // hit leaves in compacted rounds: round k tests every lane's k-th hit leaf
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (__ballot(leafm != 0) == 0) break;
+    if (leafm) {
+      const int c = __builtin_ctz(leafm);
+      leafm &= leafm - 1;
+      int cd = code[0];
+#pragma unroll
+      for (int j = 1; j < 8; j++) cd = c == j ? code[j] : cd;
+      if (leaf_test<ANY>(S, r, tmin, tmax, cd, h) && ANY) return true;
+    }
+  }
+  const float lim2 = (ANY || h.slot < 0) ? lim : h.t * 1.00001f;
+  float k[8];
+  int cnt = 0;
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    const bool in = ((hitm >> c) & 1u) && code[c] >= 0 && tn[c] <= lim2;
+    k[c] = in ? tn[c] : INFINITY;
+    cnt += in ? 1 : 0;
+  }
+  if (cnt > 0) {
+    cas8(k, code, 0, 2); cas8(k, code, 1, 3); cas8(k, code, 4, 6); cas8(k, code, 5, 7);
+    cas8(k, code, 0, 4); cas8(k, code, 1, 5); cas8(k, code, 2, 6); cas8(k, code, 3, 7);
+    cas8(k, code, 0, 1); cas8(k, code, 2, 3); cas8(k, code, 4, 5); cas8(k, code, 6, 7);
+    cas8(k, code, 2, 4); cas8(k, code, 3, 5);
+    cas8(k, code, 1, 4); cas8(k, code, 3, 6);
+    cas8(k, code, 1, 2); cas8(k, code, 3, 4); cas8(k, code, 5, 6);
+    if (sp + cnt - 1 > kStackDepth + kSpillDepth) {
+      *overflow = 1;
+    } else if (sp + cnt - 1 <= kStackDepth) {
+#pragma unroll
+      for (int j = 7; j > 0; j--)
+        if (j < cnt) stack[(sp++) * stride] = code[j];
+    } else if (kSpillDepth > 0) {
+#pragma unroll
+      for (int j = 7; j > 0; j--) {
+        if (j < cnt) {
+          if (sp < kStackDepth) stack[sp * stride] = code[j];
+          else spill[sp - kStackDepth] = code[j];
+          sp++;
+        }
+      }
+    }
+    node = code[0];
+    return false;
+  }
+  if (sp == 0) return true;
+  sp--;
+  node = (kSpillDepth == 0 || sp < kStackDepth) ? stack[sp * stride] : spill[sp - kStackDepth];
+  return false;
+}
+
+template <bool ANY>
+__device__ __forceinline__ bool traverse_step(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
+                                              int stride, int* spill, int& node, int& sp, HitInfo& h,
+                                              int* overflow) {
+  if (kBvhWidth == 8) return traverse_step8<ANY>(S, r, tmin, tmax, stack, stride, spill, node, sp, h, overflow);
+  return traverse_step4<ANY>(S, r, tmin, tmax, stack, stride, spill, node, sp, h, overflow);
 }
 
 template <bool ANY>

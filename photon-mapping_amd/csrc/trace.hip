@@ -164,7 +164,10 @@ __global__ __launch_bounds__(kTBlock) void k_ph_trace(DevScene S, const PhotonRa
 #ifndef PM_RAY_POOL
 #define PM_RAY_POOL 1
 #endif
-__global__ __launch_bounds__(kTBlock) void k_ph_trace_pool(DevScene S, const PhotonRay* __restrict__ rays, int64_t n,
+#ifndef PM_TPOOL_WAVES
+#define PM_TPOOL_WAVES 0   // occupancy target of k_ph_trace_pool (0: compiler's choice)
+#endif
+__global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TPOOL_WAVES) void k_ph_trace_pool(DevScene S, const PhotonRay* __restrict__ rays, int64_t n,
                                                            float2* __restrict__ hits, int* overflow, int chunk) {
   __shared__ int stack[kStackDepth * kTBlock];
   __shared__ int lnext;
