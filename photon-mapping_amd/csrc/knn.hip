@@ -489,9 +489,15 @@ template <int TAG, int QL, bool JUMP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
-    int64_t stride, int64_t sstride, int64_t gran) {
+    int64_t stride, int64_t sstride, int64_t gran, int xcd) {
   __shared__ double lq[QL * 256];
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // xcd (A/B knob, off): workgroups are dealt round-robin to the 8 XCDs; remap so
+  // XCD x walks the contiguous block range [x * G/8, (x+1) * G/8) (its own narrow
+  // window of the tree in its L2) instead of all XCDs sharing one window (grid
+  // padded to 8k). Measured on config 3: global gather 50.3 -> 60.4 ms, i.e. the
+  // shared window (one copy in the Infinity Cache, fed to all 8 L2s) wins.
+  const int64_t b = xcd ? (int64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
+  const int64_t t = b * blockDim.x + threadIdx.x;
   const int64_t r = level_rank(t, stride, sstride);
   const bool valid = r < nq;
   const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
@@ -732,6 +738,8 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   const int g = grid_for(nq, 256);
   const int n = (int)m->n;
   const std::vector<int64_t> lv = seed_levels();
+  const char* xenv = std::getenv("PM_GATHER_XCD");   // A/B knob: XCD-contiguous block ranges
+  const int xcd = xenv ? std::atoi(xenv) : 0;
   if ((mode == 12 || mode == 13) && nq > lv.back()) {
     const int64_t gran = lv.back();
     DevBuf<float4> lead((nq + gran - 1) / gran);
@@ -741,10 +749,11 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
       const int64_t stride = l < lv.size() ? lv[l] : 1;
       const int64_t nr = (nq + stride - 1) / stride - (sstride ? (nq + sstride - 1) / sstride : 0);
       {
-        const int gl = grid_for(nr, 256);
+        int gl = grid_for(nr, 256);
+        if (xcd) gl = (gl + 7) / 8 * 8;
 #define PM_LEVEL(T, J)                                                                                         \
   k_gather_level<T, 8, J><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, stride, \
-                                             sstride, gran)
+                                             sstride, gran, xcd)
         if (tag == 1 && mode == 13) PM_LEVEL(1, true);
         else if (tag == 1) PM_LEVEL(1, false);
         else if (mode == 13) PM_LEVEL(0, true);

@@ -483,7 +483,7 @@ def test_render_continuation_rerun(sphere, monkeypatch):
     assert np.array_equal(_bits(ra.cpu().numpy()), _bits(rb.cpu().numpy()))
 
 
-@pytest.mark.parametrize("levels", [None, "256,16", "64,8,2"])
+@pytest.mark.parametrize("levels", [None, "256,16", "64,8,2", "xcd"])
 @pytest.mark.parametrize("jitter", [0.0, 1e-3, 0.5])
 def test_seeded_gather_tight_neighbours(cornell, monkeypatch, jitter, levels):
     """Mode 12 (leader-seeded cut-offs) on queries in spatial order, where the
@@ -506,7 +506,9 @@ def test_seeded_gather_tight_neighbours(cornell, monkeypatch, jitter, levels):
     brdf = torch.from_numpy(rng.uniform(0, 0.4, size=len(q)).astype(np.float32)).cuda()
     monkeypatch.setenv("PM_GATHER_MODE", "11")
     ref = [pm_amd.gather_photons(m, qt, brdf).cpu().numpy() for m in (gm, cm)]
-    if levels:
+    if levels == "xcd":   # XCD-contiguous block ranges (PM_GATHER_XCD)
+        monkeypatch.setenv("PM_GATHER_XCD", "1")
+    elif levels:
         monkeypatch.setenv("PM_SEED_LEVELS", levels)
     for mode in ("12", "13", "14"):
         monkeypatch.setenv("PM_GATHER_MODE", mode)
