@@ -194,6 +194,29 @@ int pm_photon_map_size(const pm_photon_map* map, int64_t* n);
 int pm_photon_map_export(const pm_photon_map* map, pm_kd_photon* d_out, void* stream);
 int pm_photon_map_destroy(pm_photon_map* map);
 
+/* ---- stage 2a across G ranks (replaces the replicated buildTree)
+ * Every rank holds the same all-gathered photons (pm_photon_map_create's
+ * arguments). pm_kd_shard_plan_create selects the top L = min(ceil(log2 G) + 1, 5)
+ * levels of the global tree on every rank; the caller deals the 2^L subtrees
+ * to ranks (any deterministic assignment, e.g. balanced by size), each rank
+ * builds its own (pm_kd_shard_build, 16-B node records in the subtree's own
+ * implicit layout), the caller all-gathers them, concatenated in subtree
+ * order, and pm_photon_map_create_sharded places them. The map equals
+ * pm_photon_map_create's bit for bit. A plan with 0 subtrees (map too small
+ * to split, or G == 1) builds the whole tree in pm_photon_map_create_sharded. */
+typedef struct pm_kd_shard_plan pm_kd_shard_plan;
+int pm_kd_shard_plan_create(const pm_photon* d_a, int64_t na, float power_a,
+                            const pm_photon* d_b, int64_t nb, float power_b,
+                            int32_t world, pm_kd_shard_plan** out, void* stream);
+/* *count = number of subtrees (2^L or 0); h_sizes (count entries) may be NULL. */
+int pm_kd_shard_subtrees(const pm_kd_shard_plan* plan, int32_t* count, int64_t* h_sizes);
+int pm_kd_shard_build(pm_kd_shard_plan* plan, int32_t subtree, float* d_nodes /* 4 x size */,
+                      void* stream);
+/* d_subtrees: all subtrees' records in subtree order (NULL if count == 0). */
+int pm_photon_map_create_sharded(pm_kd_shard_plan* plan, const float* d_subtrees,
+                                 pm_photon_map** out, void* stream);
+int pm_kd_shard_plan_destroy(pm_kd_shard_plan* plan);
+
 /* ---- stage 2b: kNN + radiance estimate ----------------------------------
  * cukd::stackBased::knn<HeapCandidateList<k>> (shading.h:11-18): exact k
  * nearest photons with d^2 < max_radius^2, ordered by (d^2, original index);

@@ -453,6 +453,125 @@ int pm_photon_map_destroy(pm_photon_map* m) {
   return PM_OK;
 }
 
+// ---- sharded global-map build (kdshard.hip)
+struct pm_kd_shard_plan {
+  DevBuf<float4> elems, payload, top;
+  DevBuf<uint8_t> sub;   // subtree of every element (255: a top node)
+  int64_t n = 0;
+  int L = 0;   // 0: not split
+  std::vector<int64_t> sizes;
+};
+
+int pm_kd_shard_plan_create(const pm_photon* a, int64_t na, float pa, const pm_photon* b, int64_t nb, float pb,
+                            int32_t world, pm_kd_shard_plan** out, void* stream) {
+  if (!out || na < 0 || nb < 0 || world < 1 || (na > 0 && !a) || (nb > 0 && !b)) return PM_ERR_INVALID;
+  *out = nullptr;
+  int st = require_device();
+  if (st != PM_OK) return st;
+  const int64_t n = na + nb;
+  if (n >= (1ll << 30)) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  pm_kd_shard_plan* p = new pm_kd_shard_plan;
+  p->n = n;
+  hipError_t e = hipSuccess;
+  if (n > 0) {
+    p->elems.alloc(n);
+    p->payload.alloc(n);
+    if (!p->elems.p || !p->payload.p) {
+      delete p;
+      return PM_ERR_OOM;
+    }
+    reset_phase(PH_KDBUILD);
+    PhaseTimer tm(PH_KDBUILD, s);
+    e = launch_elems_from_photons(a, na, b, nb, pa, pb, p->elems.p, p->payload.p, s);
+    const int L = shard_levels(world);
+    if (e == hipSuccess && world > 1 && shard_ok(n, L)) {
+      p->top.alloc((size_t)1 << L);
+      if (!p->top.p) e = hipErrorOutOfMemory;
+      if (e == hipSuccess) e = kd_shard_top(p->elems.p, n, L, p->top.p, p->sizes, s);
+      if (e == hipSuccess) {
+        p->sub.alloc(n);
+        e = p->sub.p ? kd_shard_classify(p->elems.p, n, L, p->top.p, p->sub.p, s) : hipErrorOutOfMemory;
+      }
+      if (e == hipSuccess) p->L = L;
+    }
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    delete p;
+    return map_err(e);
+  }
+  *out = p;
+  return PM_OK;
+}
+
+int pm_kd_shard_subtrees(const pm_kd_shard_plan* p, int32_t* count, int64_t* sizes) {
+  if (!p || !count) return PM_ERR_INVALID;
+  *count = p->L > 0 ? (int32_t)p->sizes.size() : 0;
+  if (sizes)
+    for (int32_t j = 0; j < *count; j++) sizes[j] = p->sizes[j];
+  return PM_OK;
+}
+
+int pm_kd_shard_build(pm_kd_shard_plan* p, int32_t j, float* d_nodes, void* stream) {
+  if (!p || p->L == 0 || j < 0 || j >= (int32_t)p->sizes.size() || (p->sizes[j] > 0 && !d_nodes))
+    return PM_ERR_INVALID;
+  int st = require_device();
+  if (st != PM_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  reset_phase(PH_KDBUILD);
+  hipError_t e;
+  {
+    PhaseTimer tm(PH_KDBUILD, s);
+    e = kd_shard_subtree(p->elems.p, p->sub.p, p->n, j, p->sizes[j], reinterpret_cast<float4*>(d_nodes), s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  return map_err(e);
+}
+
+int pm_photon_map_create_sharded(pm_kd_shard_plan* p, const float* subs, pm_photon_map** out, void* stream) {
+  if (!p || !out || (p->L > 0 && !subs)) return PM_ERR_INVALID;
+  *out = nullptr;
+  int st = require_device();
+  if (st != PM_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  pm_photon_map* m = new pm_photon_map;
+  m->n = p->n;
+  hipError_t e = hipSuccess;
+  if (p->n > 0) {
+    m->nodes.alloc(p->n);
+    if (!m->nodes.p) {
+      delete m;
+      return PM_ERR_OOM;
+    }
+    reset_phase(PH_KDBUILD);
+    {
+      PhaseTimer tm(PH_KDBUILD, s);
+      if (p->L > 0)
+        e = kd_shard_assemble(p->top.p, p->L, reinterpret_cast<const float4*>(subs), p->sizes, m->nodes.p, s);
+      else
+        e = kd_build(p->elems.p, p->n, m->nodes.p, s);
+    }
+    std::swap(m->payload.p, p->payload.p);   // the plan's payload moves into the map
+    std::swap(m->payload.n, p->payload.n);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess || (p->n > 0 && !m->payload.p)) {
+    delete m;
+    return e != hipSuccess ? map_err(e) : PM_ERR_INVALID;   // a plan's payload moves once
+  }
+  *out = m;
+  return PM_OK;
+}
+
+int pm_kd_shard_plan_destroy(pm_kd_shard_plan* p) {
+  delete p;
+  return PM_OK;
+}
+
 int pm_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int32_t k, float max_radius, int32_t* ids,
            float* d2, float* maxd2, void* stream) {
   if (!m || nq < 0 || k < 1 || k > 256 || (nq > 0 && (!q || !ids)) || !(max_radius >= 0.f)) return PM_ERR_INVALID;

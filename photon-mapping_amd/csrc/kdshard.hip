@@ -1,0 +1,456 @@
+// kdshard.hip — the global map's kd-tree built across G ranks.
+//
+// The reference builds one tree on one device (cukd::buildTree, ray-tracer/
+// src/hostCode.cu:94-95). With G GPUs every rank holds the same all-gathered
+// photons, and rebuilding the whole tree on every rank (the replicated build)
+// costs N log N of the G-times-larger map: 311 ms at 8 x 45.4 M photons against
+// 35 ms for one GPU's share. Here the top L = ceil(log2 G) + 1 levels are
+// selected directly (every rank, redundantly, a few passes over the elements),
+// the 2^L subtrees below them are dealt to the ranks (balanced by size: about
+// two per rank) and built with the ordinary kd_build, and the built subtrees are
+// all-gathered and placed into the implicit layout. The
+// result is the SAME tree as kd_build over all elements (same left-balanced
+// ranks, same widest-dimension rule, same (coordinate, original index) order;
+// tested bitwise): only who computes which part changes.
+//
+//   top level l, segment j (size s): dim = widest extent of its elements (the
+//   extents kd_build reads from its presorted lists: min / max), median = the
+//   element of rank left_size(s) in (orderable_key(coord), index) order, found by
+//   an 8-bit radix select on that 64-bit key: two histogram passes over all
+//   elements, one compaction of the elements whose top 16 key bits match, six
+//   histogram passes over those candidates.
+//   subtree j: the elements whose top-level path ends at j (stable compaction,
+//   so local order = global index order and ties break the same way), built by
+//   kd_build, original indices restored.
+#include <algorithm>
+#include <cstring>
+
+#include "pm_internal.hpp"
+
+namespace pmd {
+
+constexpr int kShardMaxLevels = 5;   // <= 16 top segments per level, <= 32 subtrees
+
+static inline int left_size_host(int s) {
+  if (s <= 1) return 0;
+  const int h = 32 - __builtin_clz((unsigned)s);
+  const int half = 1 << (h - 2);
+  const int full = (1 << (h - 1)) - 1;
+  const int last = s - full;
+  return (half - 1) + std::min(last, half);
+}
+
+__device__ __forceinline__ float shard_coord(const float4 e, int d) { return d == 0 ? e.x : (d == 1 ? e.y : e.z); }
+
+// segment of e among the 2^l segments below the top l levels, or -1 if e is
+// one of the top nodes (kd_class: left iff (c, id) < (node c, node id))
+__device__ __forceinline__ int top_path(const float4 e, const float4* __restrict__ top, int l) {
+  const int id = __float_as_int(e.w);
+  int t = 0;
+  for (int k = 0; k < l; k++) {
+    const float4 nd = top[t];
+    const int w = __float_as_int(nd.w), dim = w & 3, nid = w >> 2;
+    if (id == nid) return -1;
+    const float c = shard_coord(e, dim), nc = shard_coord(nd, dim);
+    const bool left = c < nc || (c == nc && id < nid);
+    t = 2 * t + (left ? 1 : 2);
+  }
+  return t - ((1 << l) - 1);
+}
+
+__device__ __forceinline__ uint64_t shard_key(const float4 e, int dim) {
+  return ((uint64_t)orderable_key(shard_coord(e, dim)) << 32) | (uint32_t)__float_as_int(e.w);
+}
+
+// grid-stride passes over all elements: a fixed grid, one LDS init / flush per block
+constexpr int kShardGrid = 2048;
+
+// per-segment min / max of the orderable keys of x, y, z. NR > 0: the first
+// levels (<= NR segments) keep per-thread register accumulators (same-address
+// LDS atomics from a whole wave serialise: level 0 has one segment); deeper
+// levels spread over 8-16 segments and use LDS atomics. One global atomic per
+// block, segment and component.
+template <int NR>
+__global__ void k_shard_bounds(const float4* __restrict__ elems, int64_t n, const float4* __restrict__ top, int l,
+                               uint32_t* __restrict__ ob /* [nseg][6] */) {
+  __shared__ uint32_t sb[16 * 6];
+  const int nseg = 1 << l;
+  for (int k = threadIdx.x; k < nseg * 6; k += blockDim.x) sb[k] = (k % 6) < 3 ? 0xFFFFFFFFu : 0u;
+  __syncthreads();
+  uint32_t acc[NR > 0 ? NR : 1][6];
+#pragma unroll
+  for (int r = 0; r < (NR > 0 ? NR : 1); r++)
+#pragma unroll
+    for (int k = 0; k < 6; k++) acc[r][k] = k < 3 ? 0xFFFFFFFFu : 0u;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 e = elems[i];
+    const int j = top_path(e, top, l);
+    if (j < 0) continue;
+    const uint32_t k3[3] = {orderable_key(e.x), orderable_key(e.y), orderable_key(e.z)};
+    if (NR > 0) {
+#pragma unroll
+      for (int r = 0; r < NR; r++) {
+        if (j == r) {
+#pragma unroll
+          for (int d = 0; d < 3; d++) {
+            acc[r][d] = min(acc[r][d], k3[d]);
+            acc[r][3 + d] = max(acc[r][3 + d], k3[d]);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        atomicMin(&sb[6 * j + d], k3[d]);
+        atomicMax(&sb[6 * j + 3 + d], k3[d]);
+      }
+    }
+  }
+  if (NR > 0) {
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      if (r < nseg) {
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+          if (acc[r][d] != 0xFFFFFFFFu) atomicMin(&sb[6 * r + d], acc[r][d]);
+          if (acc[r][3 + d] != 0u) atomicMax(&sb[6 * r + 3 + d], acc[r][3 + d]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nseg * 6; k += blockDim.x) {
+    if ((k % 6) < 3) {
+      if (sb[k] != 0xFFFFFFFFu) atomicMin(&ob[k], sb[k]);
+    } else if (sb[k] != 0u) {
+      atomicMax(&ob[k], sb[k]);
+    }
+  }
+}
+
+struct ShardSel {
+  int dim[16];
+  uint64_t prefix[16];   // key bits above `shift + 8` selected so far
+};
+
+// segment -> (dim, prefix) in LDS (a by-value kernel argument indexed at run
+// time would go through private memory)
+struct ShardSelLds {
+  int dim[16];
+  uint64_t prefix[16];
+  __device__ __forceinline__ void load(const ShardSel& s) {
+    if (threadIdx.x < 16) {
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if ((int)threadIdx.x == k) dim[k] = s.dim[k], prefix[k] = s.prefix[k];
+    }
+  }
+};
+
+// 256-bin histogram of key bits [shift, shift + 8) over the elements of each
+// segment whose key matches the segment's prefix above them; up to two wave
+// rounds merge lanes with the same (segment, bin) before the LDS atomics
+__global__ void k_shard_hist(const float4* __restrict__ elems, int64_t n, const float4* __restrict__ top, int l,
+                             ShardSel sel, int shift, uint32_t* __restrict__ hist /* [nseg][256] */) {
+  __shared__ uint32_t sh[16 * 256];
+  __shared__ ShardSelLds ss;
+  const int nseg = 1 << l;
+  const int lane = threadIdx.x & 63;
+  for (int k = threadIdx.x; k < nseg * 256; k += blockDim.x) sh[k] = 0;
+  ss.load(sel);
+  __syncthreads();
+  const int hb = shift + 8;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += step) {
+    const int64_t i = base + threadIdx.x;
+    int slot = -1;
+    if (i < n) {
+      const float4 e = elems[i];
+      const int j = top_path(e, top, l);
+      if (j >= 0) {
+        const uint64_t key = shard_key(e, ss.dim[j]);
+        if (hb >= 64 || (key >> hb) == (ss.prefix[j] >> hb)) slot = 256 * j + (int)((key >> shift) & 255u);
+      }
+    }
+    for (int round = 0; round < 2; round++) {
+      const uint64_t pending = __ballot(slot >= 0);
+      if (!pending) break;
+      const int sl = __shfl(slot, __builtin_ctzll(pending));
+      const uint64_t m = __ballot(slot == sl);
+      if (lane == __builtin_ctzll(m)) atomicAdd(&sh[sl], (uint32_t)__popcll(m));
+      if (slot == sl) slot = -1;
+    }
+    if (slot >= 0) atomicAdd(&sh[slot], 1u);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nseg * 256; k += blockDim.x)
+    if (sh[k]) atomicAdd(&hist[k], sh[k]);
+}
+
+// the matching elements' keys, per segment, into cand[off[j] ...): block-
+// aggregated over chunks of kCompactIPT x 256 elements (LDS counts, one global
+// atomic per block, segment and chunk)
+constexpr int kCompactIPT = 8;
+__global__ void k_shard_compact(const float4* __restrict__ elems, int64_t n, const float4* __restrict__ top, int l,
+                                ShardSel sel, int hb, const uint64_t* __restrict__ off,
+                                unsigned long long* __restrict__ cnt, uint64_t* __restrict__ cand) {
+  __shared__ ShardSelLds ss;
+  __shared__ uint32_t lc[16];
+  __shared__ unsigned long long lb[16];
+  const int nseg = 1 << l;
+  ss.load(sel);
+  const int64_t chunk = (int64_t)blockDim.x * kCompactIPT;
+  for (int64_t base = (int64_t)blockIdx.x * chunk; base < n; base += (int64_t)gridDim.x * chunk) {
+    if (threadIdx.x < 16) lc[threadIdx.x] = 0;
+    __syncthreads();
+    int j[kCompactIPT];
+    uint32_t mine[kCompactIPT];
+    uint64_t key[kCompactIPT];
+#pragma unroll
+    for (int k = 0; k < kCompactIPT; k++) {
+      const int64_t i = base + k * blockDim.x + threadIdx.x;
+      j[k] = -1;
+      key[k] = 0;
+      if (i < n) {
+        const float4 e = elems[i];
+        j[k] = top_path(e, top, l);
+        if (j[k] >= 0) {
+          key[k] = shard_key(e, ss.dim[j[k]]);
+          if ((key[k] >> hb) != (ss.prefix[j[k]] >> hb)) j[k] = -1;
+        }
+      }
+      mine[k] = j[k] >= 0 ? atomicAdd(&lc[j[k]], 1u) : 0u;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nseg && lc[threadIdx.x] > 0)
+      lb[threadIdx.x] = atomicAdd(&cnt[threadIdx.x], (unsigned long long)lc[threadIdx.x]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kCompactIPT; k++)
+      if (j[k] >= 0) cand[off[j[k]] + lb[j[k]] + mine[k]] = key[k];
+  }
+}
+
+__global__ void k_shard_cand_hist(const uint64_t* __restrict__ cand, int64_t nc, uint64_t prefix, int shift,
+                                  uint32_t* __restrict__ hist /* [256] */) {
+  __shared__ uint32_t sh[256];
+  for (int k = threadIdx.x; k < 256; k += blockDim.x) sh[k] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nc) {
+    const uint64_t key = cand[i];
+    const int hb = shift + 8;
+    if ((key >> hb) == (prefix >> hb)) atomicAdd(&sh[(int)((key >> shift) & 255u)], 1u);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 256; k += blockDim.x)
+    if (sh[k]) atomicAdd(&hist[k], sh[k]);
+}
+
+// top node t = 2^l - 1 + j: the selected element, split dimension in the tag
+__global__ void k_shard_top_write(const float4* __restrict__ elems, ShardSel sel, int l, float4* __restrict__ top) {
+  const int j = threadIdx.x;
+  if (j >= (1 << l)) return;
+  const int id = (int)(uint32_t)sel.prefix[j];
+  const float4 e = elems[id];
+  top[(1 << l) - 1 + j] = make_float4(e.x, e.y, e.z, __int_as_float((id << 2) | sel.dim[j]));
+}
+
+// subtree of every element (255: a top node), once per plan
+__global__ void k_shard_sub(const float4* __restrict__ elems, int64_t n, const float4* __restrict__ top, int L,
+                            uint8_t* __restrict__ sub) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int j = top_path(elems[i], top, L);
+  sub[i] = j < 0 ? 255 : (uint8_t)j;
+}
+
+__global__ void k_shard_flags(const uint8_t* __restrict__ sub, int64_t n, int j, uint32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  flags[i] = sub[i] == j ? 1u : 0u;
+}
+
+__global__ void k_shard_extract(const float4* __restrict__ elems, int64_t n, const uint32_t* __restrict__ flags,
+                                const uint32_t* __restrict__ pos, float4* __restrict__ sub,
+                                int32_t* __restrict__ gid) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !flags[i]) return;
+  const float4 e = elems[i];
+  const uint32_t p = pos[i];
+  sub[p] = make_float4(e.x, e.y, e.z, __int_as_float((int)p));
+  gid[p] = __float_as_int(e.w);
+}
+
+__global__ void k_shard_remap(float4* __restrict__ nodes, int64_t s, const int32_t* __restrict__ gid) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= s) return;
+  const float4 nd = nodes[u];
+  const int w = __float_as_int(nd.w);
+  nodes[u] = make_float4(nd.x, nd.y, nd.z, __int_as_float((gid[w >> 2] << 2) | (w & 3)));
+}
+
+// subtree rooted at global node t: local node u (depth d, k-th at that depth)
+// -> global (t + 1) 2^d - 1 + k
+__global__ void k_shard_place(const float4* __restrict__ sub, int64_t s, int64_t t, float4* __restrict__ nodes) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= s) return;
+  const int d = 63 - __clzll((unsigned long long)(u + 1));
+  const int64_t k = u + 1 - ((int64_t)1 << d);
+  nodes[(t + 1) * ((int64_t)1 << d) - 1 + k] = sub[u];
+}
+
+// levels for G ranks: ceil(log2 G) + 1, capped: about two subtrees per rank, so
+// the caller can balance the left-balanced tree's unequal subtrees (the left
+// ones hold the full last level: up to 2x the right ones)
+int shard_levels(int world) {
+  int L = 0;
+  while ((1 << L) < world) L++;
+  return std::min(L + 1, kShardMaxLevels);
+}
+
+bool shard_ok(int64_t n, int L) { return L >= 1 && L <= kShardMaxLevels && n >= (2ll << L) && n < (1ll << 30); }
+
+// Top L levels: top[0 .. 2^L - 1) and the 2^L subtree sizes (host).
+hipError_t kd_shard_top(const float4* elems, int64_t n, int L, float4* top, std::vector<int64_t>& sizes,
+                        hipStream_t s) {
+  if (!shard_ok(n, L)) return hipErrorInvalidValue;
+  std::vector<int64_t> seg{n};
+  DevBuf<uint32_t> ob(16 * 6), hist(16 * 256);
+  DevBuf<uint64_t> off(16);
+  DevBuf<unsigned long long> cnt(16);
+  DevBuf<uint64_t> cand;
+  if (!ob.p || !hist.p || !off.p || !cnt.p) return hipErrorOutOfMemory;
+  const int g = (int)std::min<int64_t>(kShardGrid, (n + 255) / 256);
+  for (int l = 0; l < L; l++) {
+    const int nseg = 1 << l;
+    // widest dimension per segment
+    std::vector<uint32_t> hb(nseg * 6);
+    for (int k = 0; k < nseg * 6; k++) hb[k] = (k % 6) < 3 ? 0xFFFFFFFFu : 0u;
+    PM_HIP_TRY(hipMemcpyAsync(ob.p, hb.data(), 4 * hb.size(), hipMemcpyHostToDevice, s));
+    if (nseg <= 4) k_shard_bounds<4><<<g, 256, 0, s>>>(elems, n, top, l, ob.p);
+    else k_shard_bounds<0><<<g, 256, 0, s>>>(elems, n, top, l, ob.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(hipMemcpyAsync(hb.data(), ob.p, 4 * hb.size(), hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    ShardSel sel{};
+    std::vector<int64_t> rank(nseg);
+    for (int j = 0; j < nseg; j++) {
+      float ext[3];
+      for (int d = 0; d < 3; d++) {
+        auto to_f = [](uint32_t u) {
+          const uint32_t bits = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+          float f;
+          std::memcpy(&f, &bits, 4);
+          return f;
+        };
+        ext[d] = to_f(hb[6 * j + 3 + d]) - to_f(hb[6 * j + d]);   // last - first of the sorted list
+      }
+      int dim = 0;
+      if (ext[1] > ext[dim]) dim = 1;
+      if (ext[2] > ext[dim]) dim = 2;
+      sel.dim[j] = dim;
+      sel.prefix[j] = 0;
+      rank[j] = left_size_host((int)seg[j]);
+    }
+    // radix select, 8 bits per pass from the top of the 64-bit key
+    auto take = [&](const std::vector<uint32_t>& h, int j, int shift) {
+      int64_t r = rank[j];
+      int b = 0;
+      for (; b < 255; b++) {
+        if (r < (int64_t)h[256 * j + b]) break;
+        r -= h[256 * j + b];
+      }
+      rank[j] = r;
+      sel.prefix[j] |= (uint64_t)b << shift;
+      return (int64_t)h[256 * j + b];
+    };
+    std::vector<uint32_t> hh(nseg * 256);
+    std::vector<int64_t> ncand(nseg);
+    for (int pass = 0; pass < 2; pass++) {
+      const int shift = 56 - 8 * pass;
+      PM_HIP_TRY(hipMemsetAsync(hist.p, 0, 4 * 256 * nseg, s));
+      k_shard_hist<<<g, 256, 0, s>>>(elems, n, top, l, sel, shift, hist.p);
+      PM_HIP_TRY(hipGetLastError());
+      PM_HIP_TRY(hipMemcpyAsync(hh.data(), hist.p, 4 * hh.size(), hipMemcpyDeviceToHost, s));
+      PM_HIP_TRY(hipStreamSynchronize(s));
+      for (int j = 0; j < nseg; j++) ncand[j] = take(hh, j, shift);
+    }
+    std::vector<uint64_t> ho(nseg);
+    int64_t tot = 0;
+    for (int j = 0; j < nseg; j++) ho[j] = (uint64_t)tot, tot += ncand[j];
+    if ((int64_t)cand.n < tot) cand.alloc(tot);
+    if (!cand.p) return hipErrorOutOfMemory;
+    PM_HIP_TRY(hipMemcpyAsync(off.p, ho.data(), 8 * nseg, hipMemcpyHostToDevice, s));
+    PM_HIP_TRY(hipMemsetAsync(cnt.p, 0, 8 * nseg, s));
+    k_shard_compact<<<g, 256, 0, s>>>(elems, n, top, l, sel, 48, off.p, cnt.p, cand.p);
+    PM_HIP_TRY(hipGetLastError());
+    for (int pass = 2; pass < 8; pass++) {
+      const int shift = 56 - 8 * pass;
+      PM_HIP_TRY(hipMemsetAsync(hist.p, 0, 4 * 256 * nseg, s));
+      for (int j = 0; j < nseg; j++)
+        if (ncand[j] > 0)
+          k_shard_cand_hist<<<grid_for(ncand[j], 256), 256, 0, s>>>(cand.p + ho[j], ncand[j], sel.prefix[j], shift,
+                                                                     hist.p + 256 * j);
+      PM_HIP_TRY(hipGetLastError());
+      PM_HIP_TRY(hipMemcpyAsync(hh.data(), hist.p, 4 * hh.size(), hipMemcpyDeviceToHost, s));
+      PM_HIP_TRY(hipStreamSynchronize(s));
+      for (int j = 0; j < nseg; j++) take(hh, j, shift);
+    }
+    k_shard_top_write<<<1, 64, 0, s>>>(elems, sel, l, top);
+    PM_HIP_TRY(hipGetLastError());
+    std::vector<int64_t> nxt;
+    for (int j = 0; j < nseg; j++) {
+      const int64_t ls = left_size_host((int)seg[j]);
+      nxt.push_back(ls);
+      nxt.push_back(seg[j] - ls - 1);
+    }
+    seg.swap(nxt);
+  }
+  sizes = seg;
+  return hipStreamSynchronize(s);
+}
+
+// Subtree j below the top L levels, in its local implicit layout with
+// original indices in the tags (out: sizes[j] nodes).
+hipError_t kd_shard_classify(const float4* elems, int64_t n, int L, const float4* top, uint8_t* sub, hipStream_t s) {
+  k_shard_sub<<<grid_for(n, 256), 256, 0, s>>>(elems, n, top, L, sub);
+  return hipGetLastError();
+}
+
+hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, int64_t n, int j, int64_t size, float4* out,
+                            hipStream_t s) {
+  if (size <= 0) return hipSuccess;
+  DevBuf<uint32_t> flags(n), pos(n), total(1);
+  DevBuf<float4> sub(size);
+  DevBuf<int32_t> gid(size);
+  if (!flags.p || !pos.p || !total.p || !sub.p || !gid.p) return hipErrorOutOfMemory;
+  const int g = grid_for(n, 256);
+  k_shard_flags<<<g, 256, 0, s>>>(subof, n, j, flags.p);
+  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(exclusive_scan_u32(flags.p, pos.p, n, total.p, s));
+  k_shard_extract<<<g, 256, 0, s>>>(elems, n, flags.p, pos.p, sub.p, gid.p);
+  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(kd_build(sub.p, size, out, s));
+  k_shard_remap<<<grid_for(size, 256), 256, 0, s>>>(out, size, gid.p);
+  PM_HIP_TRY(hipGetLastError());
+  return hipStreamSynchronize(s);   // scratch buffers are freed on return
+}
+
+// Global layout from the top nodes and the subtrees (concatenated in j order).
+hipError_t kd_shard_assemble(const float4* top, int L, const float4* subs, const std::vector<int64_t>& sizes,
+                             float4* nodes, hipStream_t s) {
+  const int64_t ntop = (1ll << L) - 1;
+  PM_HIP_TRY(hipMemcpyAsync(nodes, top, sizeof(float4) * ntop, hipMemcpyDeviceToDevice, s));
+  int64_t off = 0;
+  for (size_t j = 0; j < sizes.size(); j++) {
+    if (sizes[j] > 0) {
+      k_shard_place<<<grid_for(sizes[j], 256), 256, 0, s>>>(subs + off, sizes[j], ntop + (int64_t)j, nodes);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    off += sizes[j];
+  }
+  return hipSuccess;
+}
+
+}  // namespace pmd

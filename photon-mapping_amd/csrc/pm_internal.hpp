@@ -66,6 +66,19 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& tri_host, hipStre
 // Writes nodes[t] = (x, y, z, bits(orig << 2 | dim)).
 hipError_t kd_build(const float4* d_elems, int64_t n, float4* d_nodes, hipStream_t s);
 
+// Sharded build of one tree (kdshard.hip).
+int shard_levels(int world);
+bool shard_ok(int64_t n, int L);
+hipError_t kd_shard_top(const float4* elems, int64_t n, int L, float4* top, std::vector<int64_t>& sizes,
+                        hipStream_t s);
+hipError_t kd_shard_classify(const float4* elems, int64_t n, int L, const float4* top, uint8_t* sub, hipStream_t s);
+hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, int64_t n, int j, int64_t size, float4* out,
+                            hipStream_t s);
+hipError_t kd_shard_assemble(const float4* top, int L, const float4* subs, const std::vector<int64_t>& sizes,
+                             float4* nodes, hipStream_t s);
+hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
+                                     float pb, float4* elems, float4* payload, hipStream_t s);
+
 // K = 50 gather (gatherPhotons) for a batch of queries.
 // tag 0: API / caustic-map launches, 1: global-map launch (separate kernel symbol for rocprof)
 hipError_t launch_gather(const pm_photon_map* m, const float4* d_query /*pos, brdf*/, int64_t nq,

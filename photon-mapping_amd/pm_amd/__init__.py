@@ -156,6 +156,12 @@ _SIGNATURES = {
     "pm_photon_map_size": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "pm_photon_map_export": (C.c_int, [_P, _P, _P]),
     "pm_photon_map_destroy": (C.c_int, [_P]),
+    "pm_kd_shard_plan_create": (C.c_int, [_P, C.c_int64, C.c_float, _P, C.c_int64, C.c_float, C.c_int32,
+                                          C.POINTER(_P), _P]),
+    "pm_kd_shard_subtrees": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
+    "pm_kd_shard_build": (C.c_int, [_P, C.c_int32, _P, _P]),
+    "pm_photon_map_create_sharded": (C.c_int, [_P, _P, C.POINTER(_P), _P]),
+    "pm_kd_shard_plan_destroy": (C.c_int, [_P]),
     "pm_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_float, _P, _P, _P, _P]),
     "pm_gather": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P]),
     "pm_camera_setup": (C.c_int, [Float3, Float3, Float3, C.c_float, C.c_int32, C.c_int32, C.POINTER(Camera)]),
@@ -461,6 +467,56 @@ class PhotonMap:
     def close(self):
         if getattr(self, "_h", None):
             _lib.pm_photon_map_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class KdShardPlan:
+    """The global map's tree split across `world` ranks (pm_kd_shard_plan_*,
+    SURVEY §8e): top levels selected here, subtree j built by rank j % world,
+    subtrees all-gathered by the caller, then `map(all_subtrees)`."""
+
+    def __init__(self, a, power_a: float, b=None, power_b: float = 0.0, world: int = 1, stream=None):
+        h = _P()
+        na = 0 if a is None else a.shape[0]
+        nb = 0 if b is None else b.shape[0]
+        _check(_lib.pm_kd_shard_plan_create(_ptr(a) if na else None, na, float(power_a), _ptr(b) if nb else None,
+                                            nb, float(power_b), int(world), C.byref(h), _stream(stream)),
+               "pm_kd_shard_plan_create")
+        self._h = h
+        self.n = na + nb
+        cnt = C.c_int32(0)
+        _check(_lib.pm_kd_shard_subtrees(h, C.byref(cnt), None), "pm_kd_shard_subtrees")
+        sizes = (C.c_int64 * max(1, cnt.value))()
+        _check(_lib.pm_kd_shard_subtrees(h, C.byref(cnt), sizes), "pm_kd_shard_subtrees")
+        self.sizes = [int(sizes[j]) for j in range(cnt.value)]   # [] : not split
+
+    def build(self, j: int, out=None, stream=None):
+        """Subtree j as (size, 4) float32 node records (its own implicit layout)."""
+        import torch
+        if out is None:
+            out = torch.empty((max(1, self.sizes[j]), 4), dtype=torch.float32, device="cuda")
+        _check(_lib.pm_kd_shard_build(self._h, int(j), _ptr(out), _stream(stream)), "pm_kd_shard_build")
+        return out[: self.sizes[j]]
+
+    def map(self, subtrees=None, stream=None) -> "PhotonMap":
+        """The photon map from all subtrees concatenated in subtree order (None when not split)."""
+        h = _P()
+        _check(_lib.pm_photon_map_create_sharded(self._h, _ptr(subtrees) if self.sizes else None, C.byref(h),
+                                                 _stream(stream)), "pm_photon_map_create_sharded")
+        m = PhotonMap.__new__(PhotonMap)
+        m._h = h
+        m.n = self.n
+        return m
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.pm_kd_shard_plan_destroy(self._h)
             self._h = None
 
     def __del__(self):

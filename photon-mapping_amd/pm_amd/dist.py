@@ -5,9 +5,15 @@ over RCCL ("nccl" backend) on MI355X, gloo on CPU for tests.
                 mode; seeds are the per-light launch ids, so the union is
                 bit-identical to the 1-GPU trace (pm_trace_params.shard_*).
   2. exchange   ONE all-gather per photon buffer (counts first, then the padded
-                buffers); rank-order concatenation reproduces the 1-GPU array.
-  3. build      every rank builds the same kd-trees (replicated; cheaper than a
-                second exchange).
+                buffers) of position + colour (24 of 40 B; nothing else reaches
+                a map); rank-order concatenation reproduces the 1-GPU array.
+  3. build      the global map's tree is split across ranks (KdShardPlan): every
+                rank selects the top ceil(log2 G) + 1 levels, the subtrees below
+                are dealt to ranks balanced by size (shard_owners), ONE
+                all-gather of the built subtrees, every rank
+                places them (the same tree bit for bit; the replicated build
+                cost N log N of the G-times-larger map: 311 ms at 8 GPUs vs 35 ms).
+                The small caustic map is built on every rank.
   4. render     16x16 image tiles dealt round robin (tile % G == r).
   5. assemble   tiles are disjoint, so an integer SUM-reduce to rank 0 merges
                 the RGBA8 image exactly.
@@ -35,6 +41,8 @@ class FrameConfig:
     # apply the %.6f photon-file round trip in memory (pm_photons_quantize), so
     # the frame equals the reference's two-process pipeline
     quantize: bool = False
+    # split the global map's kd-tree build across ranks (N > 1; identical tree)
+    shard_build: bool = True
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -62,6 +70,88 @@ def allgather_rows(t, world: int, dist):
     return torch.cat(parts)
 
 
+def pack_rows(t):
+    """pm_photon rows (n, 10) -> (n, 6): position, colour."""
+    import torch
+    return torch.cat([t[:, 0:3], t[:, 7:10]], dim=1).contiguous()
+
+
+def unpack_rows(p):
+    """(n, 6) -> pm_photon rows with direction and power zero (never read by a map)."""
+    import torch
+    t = torch.zeros((p.shape[0], 10), dtype=p.dtype, device=p.device)
+    t[:, 0:3] = p[:, 0:3]
+    t[:, 7:10] = p[:, 3:6]
+    return t
+
+
+def shard_owners(sizes, world: int):
+    """Subtree -> rank, balanced by size (largest first to the least-loaded rank,
+    ties to the lower index): deterministic, the same on every rank."""
+    load, owner = [0] * world, [0] * len(sizes)
+    for j in sorted(range(len(sizes)), key=lambda j: (-sizes[j], j)):
+        r = min(range(world), key=lambda r: (load[r], r))
+        owner[j] = r
+        load[r] += sizes[j]
+    return owner, load
+
+
+def shard_local(plan, rank: int, world: int):
+    """Rank `rank`'s subtrees (shard_owners) built back to back, in subtree order,
+    into one (m_max, 4) buffer, m_max = the largest rank's total (all-gather
+    padding); returns (buffer, kd-build us)."""
+    import torch
+    pm = _pm()
+    owner, load = shard_owners(plan.sizes, world)
+    local = torch.empty((max(1, max(load)), 4), dtype=torch.float32, device="cuda")
+    off, us = 0, 0.0
+    for j, sz in enumerate(plan.sizes):
+        if owner[j] == rank:
+            plan.build(j, out=local[off: off + sz])
+            us += pm.phase_us("kdbuild")
+            off += sz
+    return local, us
+
+
+def shard_assemble(plan, everyone, world: int):
+    """The map from the all-gathered buffers ((world * m_max, 4), rank order)."""
+    import torch
+    owner, _ = shard_owners(plan.sizes, world)
+    m_max = everyone.shape[0] // world
+    parts, offs = [], [0] * world
+    for j, sz in enumerate(plan.sizes):
+        r = owner[j]
+        parts.append(everyone[r * m_max + offs[r]: r * m_max + offs[r] + sz])
+        offs[r] += sz
+    return plan.map(torch.cat(parts))
+
+
+def sharded_map(pm, g, c, rank: int, world: int, dist):
+    """Global map (diffuse ++ caustic) built across ranks; returns (map, kd-build us
+    of this rank, the subtree all-gather included)."""
+    import torch
+    plan = pm.KdShardPlan(g, pm.PHOTON_POWER, c, pm.CAUSTICS_PHOTON_POWER, world=world)
+    us = pm.phase_us("kdbuild")
+    if not plan.sizes:   # too small to split: every rank builds the whole tree
+        m = plan.map()
+        return m, us + pm.phase_us("kdbuild")
+    local, bus = shard_local(plan, rank, world)
+    t0 = time.time()
+    everyone = torch.empty((world * local.shape[0], 4), dtype=torch.float32, device=local.device)
+    dist.all_gather_into_tensor(everyone, local)
+    torch.cuda.synchronize()
+    xus = (time.time() - t0) * 1e6
+    m = shard_assemble(plan, everyone, world)
+    us += bus + xus + pm.phase_us("kdbuild")
+    plan.close()
+    return m, us
+
+
+def _pm():
+    import pm_amd
+    return pm_amd
+
+
 class GpuBackend:
     """libpm_hip.so through pm_amd (device tensors on the current cuda device)."""
 
@@ -86,10 +176,13 @@ class GpuBackend:
     def quantize(self, t):
         return self.pm.quantize_photons(t)
 
-    def maps(self, g, c):
+    def maps(self, g, c, rank: int = 0, world: int = 1, dist=None):
         pm = self.pm
-        gm = pm.PhotonMap(g, pm.PHOTON_POWER, c, pm.CAUSTICS_PHOTON_POWER)
-        kd = pm.phase_us("kdbuild")
+        if world > 1 and self.cfg.shard_build:
+            gm, kd = sharded_map(pm, g, c, rank, world, dist)
+        else:
+            gm = pm.PhotonMap(g, pm.PHOTON_POWER, c, pm.CAUSTICS_PHOTON_POWER)
+            kd = pm.phase_us("kdbuild")
         cm = pm.PhotonMap(c, pm.CAUSTICS_PHOTON_POWER)
         self.phase["kdbuild"] = kd + pm.phase_us("kdbuild")
         return gm, cm
@@ -110,16 +203,18 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     backend.phase = {}
     g = backend.trace(False, rank, world)
     c = backend.trace(True, rank, world)
+    if backend.cfg.quantize:   # elementwise: the same before or after the exchange
+        g, c = backend.quantize(g), backend.quantize(c)
     te = time.time()
     if world > 1:
-        g = allgather_rows(g, world, dist)
-        c = allgather_rows(c, world, dist)
+        # only position and colour reach the maps (kd nodes + gather payload):
+        # 24 of the 40 bytes of a photon cross xGMI
+        g = unpack_rows(allgather_rows(pack_rows(g), world, dist))
+        c = unpack_rows(allgather_rows(pack_rows(c), world, dist))
         if g.device.type == "cuda":
             torch.cuda.synchronize()
     backend.phase["exchange"] = (time.time() - te) * 1e6
-    if backend.cfg.quantize:
-        g, c = backend.quantize(g), backend.quantize(c)
-    gm, cm = backend.maps(g, c)
+    gm, cm = backend.maps(g, c, rank, world, dist)
     rgba = backend.render(gm, cm, rank, world, rgba)
     if world > 1:
         dist.reduce(rgba, dst=0, op=dist.ReduceOp.SUM)

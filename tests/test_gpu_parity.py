@@ -514,3 +514,63 @@ def test_seeded_gather_tight_neighbours(cornell, monkeypatch, jitter, levels):
         monkeypatch.setenv("PM_GATHER_MODE", mode)
         for m, r in zip((gm, cm), ref):
             assert np.array_equal(_bits(pm_amd.gather_photons(m, qt, brdf).cpu().numpy()), _bits(r)), mode
+
+
+def _synthetic_photons(n, seed, grid=None):
+    """(n, 10) pm_photon rows; `grid` snaps positions to a coarse lattice (ties,
+    exact duplicates, -0.0 and +0.0 on the planes)."""
+    rng = np.random.default_rng(seed)
+    p = np.zeros((n, 10), np.float32)
+    pos = rng.uniform(-20, 20, size=(n, 3)).astype(np.float32)
+    if grid:
+        pos = (np.round(pos / grid) * grid).astype(np.float32)
+        pos[rng.random(n) < 0.1, 1] = -0.0
+    p[:, 0:3] = pos
+    p[:, 3:6] = rng.normal(size=(n, 3))
+    p[:, 7:10] = rng.uniform(0, 1, size=(n, 3))
+    return torch.from_numpy(p).cuda()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8, 16])
+@pytest.mark.parametrize("data", ["cornell", "ties"])
+def test_sharded_kd_build_equals_replicated(cornell, world, data):
+    """SURVEY §8e build step: top levels selected on every rank, subtree j built
+    by rank j % world, all-gathered (here: concatenated in rank order) and placed;
+    the map's kd records equal the one-device build bit for bit, and so does a
+    gather through it."""
+    import pm_amd
+    from pm_amd import dist as pmdist
+    if data == "cornell":
+        meshes, lights = cornell
+        gs = pm_amd.Scene(meshes)
+        g = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, False)
+        c = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, True)
+    else:
+        g, c = _synthetic_photons(70001, 5, grid=2.5), _synthetic_photons(999, 6, grid=2.5)
+    ref = pm_amd.PhotonMap(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER)
+    plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world)
+    L = min((world - 1).bit_length() + 1, 5)
+    assert len(plan.sizes) == 2 ** L and sum(plan.sizes) == ref.n - (2 ** L - 1)
+    owner, load = pmdist.shard_owners(plan.sizes, world)
+    assert sorted(set(owner)) == list(range(min(world, 2 ** L)))
+    bufs = [pmdist.shard_local(plan, r, world)[0] for r in range(world)]
+    m = pmdist.shard_assemble(plan, torch.cat(bufs), world)
+    assert m.n == ref.n
+    assert torch.equal(m.export().view(torch.int32), ref.export().view(torch.int32))
+    rng = np.random.default_rng(3)
+    q = torch.from_numpy(rng.uniform(-20, 20, size=(3000, 3)).astype(np.float32)).cuda()
+    brdf = torch.from_numpy(rng.uniform(0, 0.4, size=3000).astype(np.float32)).cuda()
+    assert torch.equal(pm_amd.gather_photons(m, q, brdf).view(torch.int32),
+                       pm_amd.gather_photons(ref, q, brdf).view(torch.int32))
+
+
+def test_sharded_kd_build_small_map():
+    """A map too small to split (n < 2^(L+1)) is built whole by every rank."""
+    from pm_amd import dist as pmdist
+    assert pmdist.shard_owners([5, 9, 9, 3], 2) == ([0, 0, 1, 1], [14, 12])
+    import pm_amd
+    g, c = _synthetic_photons(9, 1), _synthetic_photons(3, 2)
+    plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=8)
+    assert plan.sizes == []
+    ref = pm_amd.PhotonMap(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER)
+    assert torch.equal(plan.map().export().view(torch.int32), ref.export().view(torch.int32))

@@ -1,0 +1,55 @@
+"""kd-build time vs map size on one GPU (what every rank pays per frame at N GPUs
+under the replicated build): synthetic photons uniform in a box, N = k x 45.4M."""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "photon-mapping_amd"))
+import torch
+import pm_amd
+torch.cuda.set_device(0)
+base = 45_427_140
+for k in [int(x) for x in os.environ.get("KS", "1 2 4 8").split()]:
+    n = base * k
+    g = torch.rand((n, 10), device="cuda", dtype=torch.float32) * 100.0
+    c = torch.empty((0, 10), device="cuda", dtype=torch.float32)
+    for rep in range(2):
+        torch.cuda.synchronize()
+        t0 = time.time()
+        m = pm_amd.PhotonMap(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER)
+        torch.cuda.synchronize()
+        print(f"N={n} ({k}x) kdbuild {pm_amd.phase_us('kdbuild') / 1e3:.1f} ms wall {(time.time() - t0) * 1e3:.1f} ms",
+              flush=True)
+        del m
+    del g
+    torch.cuda.empty_cache()
+
+# sharded build (pm_amd.dist.sharded_map without the collective): per-rank
+# critical path = plan (top selection) + its subtree + placement
+if os.environ.get("SHARD", "1") == "1":
+    from pm_amd import dist as pmdist
+    for k in [int(x) for x in os.environ.get("KS", "1 2 4 8").split()]:
+        world = k
+        if world < 2:
+            continue
+        n = base * k
+        g = torch.rand((n, 10), device="cuda", dtype=torch.float32) * 100.0
+        c = torch.empty((0, 10), device="cuda", dtype=torch.float32)
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = time.time()
+            plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world)
+            t_plan = pm_amd.phase_us("kdbuild") / 1e3
+            bufs, t_sub = [], []
+            for r in range(world):
+                b, us = pmdist.shard_local(plan, r, world)
+                bufs.append(b)
+                t_sub.append(us / 1e3)
+            everyone = torch.cat(bufs)
+            m = pmdist.shard_assemble(plan, everyone, world)
+            t_asm = pm_amd.phase_us("kdbuild") / 1e3
+            torch.cuda.synchronize()
+            print(f"N={n} world={world} plan {t_plan:.1f} ms, subtree max {max(t_sub):.1f} ms, place {t_asm:.1f} ms"
+                  f" -> per-rank {t_plan + max(t_sub) + t_asm:.1f} ms (+ all-gather of {everyone.numel() * 4 / 1e9:.2f} GB)",
+                  flush=True)
+            del plan, bufs, everyone, m
+        del g
+        torch.cuda.empty_cache()
