@@ -348,8 +348,10 @@ int pm_trace_photons(pm_scene* sc, const pm_light* lights, int32_t nl, const pm_
   if (!dl.p || !dloff.p) return PM_ERR_OOM;
   PM_TRY_ST(hipMemcpyAsync(dl.p, lh.data(), sizeof(LightDev) * nl, hipMemcpyHostToDevice, s));
   PM_TRY_ST(hipMemcpyAsync(dloff.p, loff.data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
-  // chunk so that the deposit slots stay below ~3 GB
-  int64_t chunk = std::min<int64_t>(np_total, std::max<int64_t>(1 << 16, (int64_t)3e9 / (40ll * per)));
+  // chunk so that the deposit slots stay below ~16 GB (of 288): config 3's 10 M
+  // photons run as ONE chunk (at ~3 GB they ran as 8.3 M + 1.7 M, and the small
+  // chunk's late bounces could not fill the GPU)
+  int64_t chunk = std::min<int64_t>(np_total, std::max<int64_t>(1 << 16, (int64_t)16e9 / (40ll * per)));
   chunk = std::min<int64_t>(chunk, 1ll << 26);
   DevBuf<pm_photon> slots((size_t)chunk * per);
   DevBuf<uint32_t> cnt(chunk), off(chunk), tot(1);
