@@ -199,9 +199,10 @@ int pm_photon_map_destroy(pm_photon_map* map);
  * arguments). pm_kd_shard_plan_create selects the top L = min(ceil(log2 G) + 1, 5)
  * levels of the global tree on every rank; the caller deals the 2^L subtrees
  * to ranks (any deterministic assignment, e.g. balanced by size), each rank
- * builds its own (pm_kd_shard_build, 16-B node records in the subtree's own
- * implicit layout), the caller all-gathers them, concatenated in subtree
- * order, and pm_photon_map_create_sharded places them. The map equals
+ * builds its own (pm_kd_shard_build: one 4-B tag per node, original index << 2
+ * | split dimension, in the subtree's own implicit layout), the caller
+ * all-gathers them, concatenated in subtree order, and
+ * pm_photon_map_create_sharded places them (positions from the photons). The map equals
  * pm_photon_map_create's bit for bit. A plan with 0 subtrees (map too small
  * to split, or G == 1) builds the whole tree in pm_photon_map_create_sharded. */
 typedef struct pm_kd_shard_plan pm_kd_shard_plan;
@@ -210,10 +211,10 @@ int pm_kd_shard_plan_create(const pm_photon* d_a, int64_t na, float power_a,
                             int32_t world, pm_kd_shard_plan** out, void* stream);
 /* *count = number of subtrees (2^L or 0); h_sizes (count entries) may be NULL. */
 int pm_kd_shard_subtrees(const pm_kd_shard_plan* plan, int32_t* count, int64_t* h_sizes);
-int pm_kd_shard_build(pm_kd_shard_plan* plan, int32_t subtree, float* d_nodes /* 4 x size */,
+int pm_kd_shard_build(pm_kd_shard_plan* plan, int32_t subtree, int32_t* d_tags /* size */,
                       void* stream);
-/* d_subtrees: all subtrees' records in subtree order (NULL if count == 0). */
-int pm_photon_map_create_sharded(pm_kd_shard_plan* plan, const float* d_subtrees,
+/* d_tags: all subtrees' tags in subtree order (NULL if count == 0). */
+int pm_photon_map_create_sharded(pm_kd_shard_plan* plan, const int32_t* d_tags,
                                  pm_photon_map** out, void* stream);
 int pm_kd_shard_plan_destroy(pm_kd_shard_plan* plan);
 

@@ -516,8 +516,8 @@ int pm_kd_shard_subtrees(const pm_kd_shard_plan* p, int32_t* count, int64_t* siz
   return PM_OK;
 }
 
-int pm_kd_shard_build(pm_kd_shard_plan* p, int32_t j, float* d_nodes, void* stream) {
-  if (!p || p->L == 0 || j < 0 || j >= (int32_t)p->sizes.size() || (p->sizes[j] > 0 && !d_nodes))
+int pm_kd_shard_build(pm_kd_shard_plan* p, int32_t j, int32_t* d_tags, void* stream) {
+  if (!p || p->L == 0 || j < 0 || j >= (int32_t)p->sizes.size() || (p->sizes[j] > 0 && !d_tags))
     return PM_ERR_INVALID;
   int st = require_device();
   if (st != PM_OK) return st;
@@ -527,13 +527,13 @@ int pm_kd_shard_build(pm_kd_shard_plan* p, int32_t j, float* d_nodes, void* stre
   hipError_t e;
   {
     PhaseTimer tm(PH_KDBUILD, s);
-    e = kd_shard_subtree(p->elems.p, p->sub.p, p->n, j, p->sizes[j], reinterpret_cast<float4*>(d_nodes), s);
+    e = kd_shard_subtree(p->elems.p, p->sub.p, p->n, j, p->sizes[j], d_tags, s);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   return map_err(e);
 }
 
-int pm_photon_map_create_sharded(pm_kd_shard_plan* p, const float* subs, pm_photon_map** out, void* stream) {
+int pm_photon_map_create_sharded(pm_kd_shard_plan* p, const int32_t* subs, pm_photon_map** out, void* stream) {
   if (!p || !out || (p->L > 0 && !subs)) return PM_ERR_INVALID;
   *out = nullptr;
   int st = require_device();
@@ -553,7 +553,7 @@ int pm_photon_map_create_sharded(pm_kd_shard_plan* p, const float* subs, pm_phot
     {
       PhaseTimer tm(PH_KDBUILD, s);
       if (p->L > 0)
-        e = kd_shard_assemble(p->top.p, p->L, reinterpret_cast<const float4*>(subs), p->sizes, m->nodes.p, s);
+        e = kd_shard_assemble(p->elems.p, p->top.p, p->L, subs, p->sizes, m->nodes.p, s);
       else
         e = kd_build(p->elems.p, p->n, m->nodes.p, s);
     }

@@ -7,8 +7,10 @@
 // 35 ms for one GPU's share. Here the top L = ceil(log2 G) + 1 levels are
 // selected directly (every rank, redundantly, a few passes over the elements),
 // the 2^L subtrees below them are dealt to the ranks (balanced by size: about
-// two per rank) and built with the ordinary kd_build, and the built subtrees are
-// all-gathered and placed into the implicit layout. The
+// two per rank) and built with the ordinary kd_build, and the built subtrees
+// (4-B tags per node: original index << 2 | split dimension) are all-gathered
+// and placed into the implicit layout, positions taken from the photons every
+// rank already holds. The
 // result is the SAME tree as kd_build over all elements (same left-balanced
 // ranks, same widest-dimension rule, same (coordinate, original index) order;
 // tested bitwise): only who computes which part changes.
@@ -282,22 +284,27 @@ __global__ void k_shard_extract(const float4* __restrict__ elems, int64_t n, con
   gid[p] = __float_as_int(e.w);
 }
 
-__global__ void k_shard_remap(float4* __restrict__ nodes, int64_t s, const int32_t* __restrict__ gid) {
+// built subtree -> 4-B tags (original index << 2 | split dimension): the
+// positions travel once, in the photon exchange, not again with the tree
+__global__ void k_shard_tags(const float4* __restrict__ nodes, int64_t s, const int32_t* __restrict__ gid,
+                             int32_t* __restrict__ tags) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= s) return;
-  const float4 nd = nodes[u];
-  const int w = __float_as_int(nd.w);
-  nodes[u] = make_float4(nd.x, nd.y, nd.z, __int_as_float((gid[w >> 2] << 2) | (w & 3)));
+  const int w = __float_as_int(nodes[u].w);
+  tags[u] = (gid[w >> 2] << 2) | (w & 3);
 }
 
 // subtree rooted at global node t: local node u (depth d, k-th at that depth)
-// -> global (t + 1) 2^d - 1 + k
-__global__ void k_shard_place(const float4* __restrict__ sub, int64_t s, int64_t t, float4* __restrict__ nodes) {
+// -> global (t + 1) 2^d - 1 + k; the position comes from elems[original index]
+__global__ void k_shard_place(const float4* __restrict__ elems, const int32_t* __restrict__ tags, int64_t s,
+                              int64_t t, float4* __restrict__ nodes) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= s) return;
   const int d = 63 - __clzll((unsigned long long)(u + 1));
   const int64_t k = u + 1 - ((int64_t)1 << d);
-  nodes[(t + 1) * ((int64_t)1 << d) - 1 + k] = sub[u];
+  const int w = tags[u];
+  const float4 e = elems[w >> 2];
+  nodes[(t + 1) * ((int64_t)1 << d) - 1 + k] = make_float4(e.x, e.y, e.z, __int_as_float(w));
 }
 
 // levels for G ranks: ceil(log2 G) + 1, capped: about two subtrees per rank, so
@@ -418,34 +425,34 @@ hipError_t kd_shard_classify(const float4* elems, int64_t n, int L, const float4
   return hipGetLastError();
 }
 
-hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, int64_t n, int j, int64_t size, float4* out,
-                            hipStream_t s) {
+hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, int64_t n, int j, int64_t size,
+                            int32_t* out, hipStream_t s) {
   if (size <= 0) return hipSuccess;
   DevBuf<uint32_t> flags(n), pos(n), total(1);
-  DevBuf<float4> sub(size);
+  DevBuf<float4> sub(size), nodes(size);
   DevBuf<int32_t> gid(size);
-  if (!flags.p || !pos.p || !total.p || !sub.p || !gid.p) return hipErrorOutOfMemory;
+  if (!flags.p || !pos.p || !total.p || !sub.p || !nodes.p || !gid.p) return hipErrorOutOfMemory;
   const int g = grid_for(n, 256);
   k_shard_flags<<<g, 256, 0, s>>>(subof, n, j, flags.p);
   PM_HIP_TRY(hipGetLastError());
   PM_HIP_TRY(exclusive_scan_u32(flags.p, pos.p, n, total.p, s));
   k_shard_extract<<<g, 256, 0, s>>>(elems, n, flags.p, pos.p, sub.p, gid.p);
   PM_HIP_TRY(hipGetLastError());
-  PM_HIP_TRY(kd_build(sub.p, size, out, s));
-  k_shard_remap<<<grid_for(size, 256), 256, 0, s>>>(out, size, gid.p);
+  PM_HIP_TRY(kd_build(sub.p, size, nodes.p, s));
+  k_shard_tags<<<grid_for(size, 256), 256, 0, s>>>(nodes.p, size, gid.p, out);
   PM_HIP_TRY(hipGetLastError());
   return hipStreamSynchronize(s);   // scratch buffers are freed on return
 }
 
-// Global layout from the top nodes and the subtrees (concatenated in j order).
-hipError_t kd_shard_assemble(const float4* top, int L, const float4* subs, const std::vector<int64_t>& sizes,
-                             float4* nodes, hipStream_t s) {
+// Global layout from the top nodes and the subtrees' tags (concatenated in j order).
+hipError_t kd_shard_assemble(const float4* elems, const float4* top, int L, const int32_t* tags,
+                             const std::vector<int64_t>& sizes, float4* nodes, hipStream_t s) {
   const int64_t ntop = (1ll << L) - 1;
   PM_HIP_TRY(hipMemcpyAsync(nodes, top, sizeof(float4) * ntop, hipMemcpyDeviceToDevice, s));
   int64_t off = 0;
   for (size_t j = 0; j < sizes.size(); j++) {
     if (sizes[j] > 0) {
-      k_shard_place<<<grid_for(sizes[j], 256), 256, 0, s>>>(subs + off, sizes[j], ntop + (int64_t)j, nodes);
+      k_shard_place<<<grid_for(sizes[j], 256), 256, 0, s>>>(elems, tags + off, sizes[j], ntop + (int64_t)j, nodes);
       PM_HIP_TRY(hipGetLastError());
     }
     off += sizes[j];

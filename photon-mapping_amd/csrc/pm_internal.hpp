@@ -72,10 +72,10 @@ bool shard_ok(int64_t n, int L);
 hipError_t kd_shard_top(const float4* elems, int64_t n, int L, float4* top, std::vector<int64_t>& sizes,
                         hipStream_t s);
 hipError_t kd_shard_classify(const float4* elems, int64_t n, int L, const float4* top, uint8_t* sub, hipStream_t s);
-hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, int64_t n, int j, int64_t size, float4* out,
-                            hipStream_t s);
-hipError_t kd_shard_assemble(const float4* top, int L, const float4* subs, const std::vector<int64_t>& sizes,
-                             float4* nodes, hipStream_t s);
+hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, int64_t n, int j, int64_t size,
+                            int32_t* out, hipStream_t s);
+hipError_t kd_shard_assemble(const float4* elems, const float4* top, int L, const int32_t* tags,
+                             const std::vector<int64_t>& sizes, float4* nodes, hipStream_t s);
 hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
                                      float pb, float4* elems, float4* payload, hipStream_t s);
 

@@ -497,15 +497,16 @@ class KdShardPlan:
         self.sizes = [int(sizes[j]) for j in range(cnt.value)]   # [] : not split
 
     def build(self, j: int, out=None, stream=None):
-        """Subtree j as (size, 4) float32 node records (its own implicit layout)."""
+        """Subtree j as (size,) int32 node tags, original index << 2 | split dim
+        (its own implicit layout)."""
         import torch
         if out is None:
-            out = torch.empty((max(1, self.sizes[j]), 4), dtype=torch.float32, device="cuda")
+            out = torch.empty((max(1, self.sizes[j]),), dtype=torch.int32, device="cuda")
         _check(_lib.pm_kd_shard_build(self._h, int(j), _ptr(out), _stream(stream)), "pm_kd_shard_build")
         return out[: self.sizes[j]]
 
     def map(self, subtrees=None, stream=None) -> "PhotonMap":
-        """The photon map from all subtrees concatenated in subtree order (None when not split)."""
+        """The photon map from all subtrees' tags concatenated in subtree order (None when not split)."""
         h = _P()
         _check(_lib.pm_photon_map_create_sharded(self._h, _ptr(subtrees) if self.sizes else None, C.byref(h),
                                                  _stream(stream)), "pm_photon_map_create_sharded")

@@ -10,7 +10,8 @@ over RCCL ("nccl" backend) on MI355X, gloo on CPU for tests.
   3. build      the global map's tree is split across ranks (KdShardPlan): every
                 rank selects the top ceil(log2 G) + 1 levels, the subtrees below
                 are dealt to ranks balanced by size (shard_owners), ONE
-                all-gather of the built subtrees, every rank
+                all-gather of the built subtrees (4-B node tags: positions come
+                from the photons already exchanged), every rank
                 places them (the same tree bit for bit; the replicated build
                 cost N log N of the G-times-larger map: 311 ms at 8 GPUs vs 35 ms).
                 The small caustic map is built on every rank.
@@ -98,12 +99,12 @@ def shard_owners(sizes, world: int):
 
 def shard_local(plan, rank: int, world: int):
     """Rank `rank`'s subtrees (shard_owners) built back to back, in subtree order,
-    into one (m_max, 4) buffer, m_max = the largest rank's total (all-gather
-    padding); returns (buffer, kd-build us)."""
+    into one (m_max,) int32 tag buffer, m_max = the largest rank's total
+    (all-gather padding); returns (buffer, kd-build us)."""
     import torch
     pm = _pm()
     owner, load = shard_owners(plan.sizes, world)
-    local = torch.empty((max(1, max(load)), 4), dtype=torch.float32, device="cuda")
+    local = torch.empty((max(1, max(load)),), dtype=torch.int32, device="cuda")
     off, us = 0, 0.0
     for j, sz in enumerate(plan.sizes):
         if owner[j] == rank:
@@ -114,7 +115,7 @@ def shard_local(plan, rank: int, world: int):
 
 
 def shard_assemble(plan, everyone, world: int):
-    """The map from the all-gathered buffers ((world * m_max, 4), rank order)."""
+    """The map from the all-gathered tag buffers ((world * m_max,), rank order)."""
     import torch
     owner, _ = shard_owners(plan.sizes, world)
     m_max = everyone.shape[0] // world
@@ -137,7 +138,7 @@ def sharded_map(pm, g, c, rank: int, world: int, dist):
         return m, us + pm.phase_us("kdbuild")
     local, bus = shard_local(plan, rank, world)
     t0 = time.time()
-    everyone = torch.empty((world * local.shape[0], 4), dtype=torch.float32, device=local.device)
+    everyone = torch.empty((world * local.shape[0],), dtype=torch.int32, device=local.device)
     dist.all_gather_into_tensor(everyone, local)
     torch.cuda.synchronize()
     xus = (time.time() - t0) * 1e6
