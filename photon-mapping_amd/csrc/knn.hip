@@ -437,6 +437,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
 #ifndef PM_SEED_STRIDE
 #define PM_SEED_STRIDE 16
 #endif
+#ifndef PM_GATHER_QL
+#define PM_GATHER_QL 8   // LDS insert-queue depth of the seeded gather (build knob)
+#endif
 #ifndef PM_SEED_LEADERS
 #define PM_SEED_LEADERS 4
 #endif
@@ -752,7 +755,7 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
         int gl = grid_for(nr, 256);
         if (xcd) gl = (gl + 7) / 8 * 8;
 #define PM_LEVEL(T, J)                                                                                         \
-  k_gather_level<T, 8, J><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, stride, \
+  k_gather_level<T, PM_GATHER_QL, J><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, stride, \
                                              sstride, gran, xcd)
         if (tag == 1 && mode == 13) PM_LEVEL(1, true);
         else if (tag == 1) PM_LEVEL(1, false);
