@@ -13,6 +13,8 @@ k = 50, max_depth 10. value = emitted photons of the whole job / wall time of
 a step (Mphotons/s traced + gathered). N > 1: photon-index sharding with a
 single all-gather, replicated kd-tree build, 16x16-tile-sharded final gather,
 image reduce to rank 0 ("weak": photons per GPU fixed, config 4 at N = 8).
+--config 5: the caustics pass (square area light + glass, 6.25M caustic photons
+per GPU = 50M at N = 8, caustic gather over k = 200); the default line is config 3.
 """
 import argparse
 import json
@@ -65,7 +67,7 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
     r0 = args.height // 2 - rows // 2
     t = time.time()
     oracle.render(sc, cam, args.width, args.height, args.spp, args.depth, SKY, lights, gm, cm,
-                  rows=(r0, r0 + rows), nthreads=nthreads)
+                  rows=(r0, r0 + rows), nthreads=nthreads, caustic_k=args.caustic_k)
     t_render = (time.time() - t) * args.height / rows
     total = t_trace + t_build + t_render
     return {
@@ -84,8 +86,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=3, choices=[3, 5],
+                    help="3: Sponza-class, 10M + 1M photons per GPU (the headline line); 5: caustics pass, "
+                         "square area light + glass, 6.25M caustic photons per GPU (50M at 8), k = 200")
     ap.add_argument("--casted", type=int, default=10_000_000, help="diffuse photons per GPU")
-    ap.add_argument("--caustic", type=int, default=1_000_000, help="caustic photons per GPU")
+    ap.add_argument("--caustic", type=int, default=None, help="caustic photons per GPU (config 3: 1M, 5: 6.25M)")
+    ap.add_argument("--caustic-k", type=int, default=None, help="caustic gather neighbours (config 3: 50, 5: 200)")
     ap.add_argument("--max-depth", type=int, default=10)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -97,6 +103,10 @@ def main():
     ap.add_argument("--cpu-sample-photons", type=int, default=2_000_000)
     ap.add_argument("--cpu-sample-rows", type=int, default=48)
     args = ap.parse_args()
+    if args.caustic is None:
+        args.caustic = 6_250_000 if args.config == 5 else 1_000_000
+    if args.caustic_k is None:
+        args.caustic_k = 200 if args.config == 5 else 50
 
     import torch
     import pm_amd
@@ -113,7 +123,10 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    if args.scene == "sponza":
+    if args.scene == "sponza" and args.config == 5:
+        meshes, lights = scenes.sponza_caustics()
+        scene_name = "sponza-class procedural, square area light + glass spheres (pm_amd.scenes.sponza_caustics)"
+    elif args.scene == "sponza":
         obj = os.environ.get("PM_SPONZA_OBJ")
         if obj and os.path.exists(obj):
             meshes, lights = pm_amd.load_scene_file(obj)
@@ -139,7 +152,7 @@ def main():
     info = {}
     cfg = pmdist.FrameConfig(casted=casted_total, caustic=caustic_total, max_depth=args.max_depth,
                              width=args.width, height=args.height, spp=args.spp, depth=args.depth, sky=SKY,
-                             camera=CAMERA)
+                             camera=CAMERA, caustic_k=args.caustic_k)
     backend = pmdist.GpuBackend(scene, lights, cfg, rank, world, gbuf=gbuf, cbuf=cbuf)
 
     def step():
@@ -202,8 +215,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (procedural Sponza-class scene; photons from the reference's own emission model)",
-        "config": {"workload": f"config3: {scene_name}, {casted_total} diffuse + {caustic_total} caustic photons, "
-                               f"{args.width}x{args.height} spp {args.spp}, depth {args.depth}, k 50",
+        "config": {"workload": f"config{args.config}: {scene_name}, {casted_total} diffuse + {caustic_total} "
+                               f"caustic photons, {args.width}x{args.height} spp {args.spp}, depth {args.depth}, "
+                               f"k 50 (caustic gather k {args.caustic_k})",
                    "triangles": ntri, "parallelism": f"photon-shard{world}+tile{world}" if world > 1 else "1 GPU"},
         "ms_per_frame": round(ms_per_step, 3),
         "mphotons_traced_per_s": round(emitted / (us["trace"] * 1e-6) / 1e6, 3) if us["trace"] else None,

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 1
+#define PM_ABI_VERSION 2
 
 enum pm_status {
   PM_OK = 0,
@@ -229,6 +229,10 @@ int pm_knn(const pm_photon_map* map, const pm_float3* d_queries, int64_t nq,
 /* gatherPhotons (shading.h:93-121), k = 50, radius 100, cone filter 1.1. */
 int pm_gather(const pm_photon_map* map, const pm_float3* d_points,
               const float* d_brdf, int64_t nq, pm_float3* d_out, void* stream);
+/* The same estimate over the k nearest (1 <= k <= 256; SURVEY §8d config 5
+ * gathers caustics with k = 200). k = 50 is pm_gather. */
+int pm_gather_k(const pm_photon_map* map, const pm_float3* d_points,
+                const float* d_brdf, int64_t nq, int32_t k, pm_float3* d_out, void* stream);
 
 /* ---- stage 2c: render (simpleRayGen, ray-tracer/cuda/deviceCode.cu:25-231) */
 typedef struct {
@@ -239,6 +243,8 @@ typedef struct {
   pm_float3 sky_colour;        /* ray-tracer.sky_colour */
   int32_t tile_rank;           /* image-tile sharding (16x16 tiles round robin) */
   int32_t tile_count;          /* 1 = whole image */
+  int32_t caustic_k;           /* neighbours of the caustic gather: 0 = the reference's
+                                  K = 50 (shading.h:7); up to 256 (config 5: 200) */
 } pm_render_params;
 
 /* setupCamera (ray-tracer/src/hostCode.cu:100-108), cos(fovy) scaling kept. */

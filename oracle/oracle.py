@@ -58,7 +58,7 @@ class TraceParams(C.Structure):
 class RenderParams(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("samples_per_pixel", C.c_int32),
                 ("max_depth", C.c_int32), ("camera", Camera), ("sky_colour", Float3),
-                ("tile_rank", C.c_int32), ("tile_count", C.c_int32)]
+                ("tile_rank", C.c_int32), ("tile_count", C.c_int32), ("caustic_k", C.c_int32)]
 
 
 class RenderStats(C.Structure):
@@ -99,6 +99,7 @@ def _load():
         "orc_map_destroy": (None, [_P]),
         "orc_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_float, C.c_int32, _P, _P, _P]),
         "orc_gather": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, _P]),
+        "orc_gather_k": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P]),
         "orc_camera_setup": (C.c_int, [Float3, Float3, Float3, C.c_float, C.c_int32, C.c_int32,
                                        C.POINTER(Camera)]),
         "orc_render": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Light), C.c_int32, _P, _P, C.c_int32,
@@ -235,12 +236,12 @@ class PhotonMap:
                          d2.ctypes.data, md.ctypes.data), "knn")
         return ids, d2, md
 
-    def gather(self, pts: np.ndarray, brdf: np.ndarray, nthreads=8):
+    def gather(self, pts: np.ndarray, brdf: np.ndarray, nthreads=8, k=50):
         pts = np.ascontiguousarray(pts, np.float32)
         brdf = np.ascontiguousarray(brdf, np.float32)
         out = np.zeros((len(pts), 3), np.float32)
-        _chk(lib.orc_gather(self.h, pts.ctypes.data, brdf.ctypes.data, len(pts), nthreads, out.ctypes.data),
-             "gather")
+        _chk(lib.orc_gather_k(self.h, pts.ctypes.data, brdf.ctypes.data, len(pts), int(k), nthreads,
+                              out.ctypes.data), "gather")
         return out
 
     def __del__(self):
@@ -257,8 +258,9 @@ def camera_setup(look_from, look_at, look_up, fovy, w, h) -> Camera:
 
 
 def render(scene: Scene, camera: Camera, w, h, spp, depth, sky, lights, gmap: PhotonMap, cmap: PhotonMap,
-           rows=None, tile_rank=0, tile_count=1, nthreads=8):
-    p = RenderParams(int(w), int(h), int(spp), int(depth), camera, _f3(sky), int(tile_rank), int(tile_count))
+           rows=None, tile_rank=0, tile_count=1, nthreads=8, caustic_k=0):
+    p = RenderParams(int(w), int(h), int(spp), int(depth), camera, _f3(sky), int(tile_rank), int(tile_count),
+                     int(caustic_k))
     rgba = np.zeros((h, w), np.uint32)
     rgb = np.zeros((h, w, 3), np.float32)
     st = RenderStats()

@@ -844,12 +844,13 @@ int orc_knn(const orc_map* m, const pm_float3* q, int64_t nq, int32_t k, float m
   return PM_OK;
 }
 
-/* shading.h:93-121 gatherPhotons; sum in (d^2, id) order */
-static v3 gather_one(const orc_map* m, v3 hit, float brdf, cand* buf) {
+/* shading.h:93-121 gatherPhotons; sum in (d^2, id) order. k = K_NEAREST is the
+ * reference's; config 5 gathers caustics over k = 200. */
+static v3 gather_one_k(const orc_map* m, v3 hit, float brdf, int k, cand* buf) {
   float q[3] = {hit.x, hit.y, hit.z};
-  const float r2 = knn_one(m, q, K_NEAREST, K_MAX_DISTANCE, buf);
+  const float r2 = knn_one(m, q, k, K_MAX_DISTANCE, buf);
   v3 flux = V3(0.f, 0.f, 0.f);
-  for (int p = 0; p < K_NEAREST; p++) {
+  for (int p = 0; p < k; p++) {
     const int32_t id = buf[p].id;
     if (id < 0 || id > m->n) continue;
     const float power = m->pw[id];
@@ -861,17 +862,25 @@ static v3 gather_one(const orc_map* m, v3 hit, float brdf, cand* buf) {
   }
   return divf(flux, (1 - (2.f / 3.f) * (1.f / CONE_FILTER_C)) * 2 * PI_F * r2);
 }
-typedef struct { const orc_map* m; const pm_float3* p; const float* brdf; pm_float3* out; } gather_ctx;
+static v3 gather_one(const orc_map* m, v3 hit, float brdf, cand* buf) {
+  return gather_one_k(m, hit, brdf, K_NEAREST, buf);
+}
+typedef struct { const orc_map* m; const pm_float3* p; const float* brdf; pm_float3* out; int k; } gather_ctx;
 static void gather_range(void* vc, int64_t lo, int64_t hi) {
   gather_ctx* c = (gather_ctx*)vc;
-  cand buf[K_NEAREST];
-  for (int64_t i = lo; i < hi; i++) c->out[i] = top3(gather_one(c->m, fromp(c->p[i]), c->brdf[i], buf));
+  cand buf[256];
+  for (int64_t i = lo; i < hi; i++) c->out[i] = top3(gather_one_k(c->m, fromp(c->p[i]), c->brdf[i], c->k, buf));
+}
+int orc_gather_k(const orc_map* m, const pm_float3* pts, const float* brdf, int64_t nq, int32_t k,
+                 int32_t nthreads, pm_float3* out) {
+  if (!m || k < 1 || k > 256) return PM_ERR_INVALID;
+  gather_ctx c = {m, pts, brdf, out, k};
+  parallel_for(nq, 256, nthreads, gather_range, &c);
+  return PM_OK;
 }
 int orc_gather(const orc_map* m, const pm_float3* pts, const float* brdf, int64_t nq,
                int32_t nthreads, pm_float3* out) {
-  gather_ctx c = {m, pts, brdf, out};
-  parallel_for(nq, 256, nthreads, gather_range, &c);
-  return PM_OK;
+  return orc_gather_k(m, pts, brdf, nq, K_NEAREST, nthreads, out);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -955,7 +964,8 @@ static v3 ray_colour(const rctx* R, v3 ro, v3 rd, prd_t* prd, cand* buf, pm_rend
   }
   const v3 direct_term = mulv(albedo, direct);
   if (st) st->caustic_queries++;
-  const v3 caustics = gather_one(R->c, prd->hr.hitpoint, diffuse_brdf, buf);
+  const v3 caustics = gather_one_k(R->c, prd->hr.hitpoint, diffuse_brdf,
+                                   R->p->caustic_k > 0 ? R->p->caustic_k : K_NEAREST, buf);
   v3 diffuse = V3(0.f, 0.f, 0.f);
   for (int s = 0; s < NUM_DIFFUSE_SAMPLES && diffuse_brdf > 0.f; s++) {
     const v3 n = normalize(prd->hr.normal);

@@ -67,6 +67,8 @@ int orc_knn(const orc_map* m, const pm_float3* q, int64_t nq, int32_t k,
             float max_radius, int32_t nthreads, int32_t* ids, float* d2, float* maxd2);
 int orc_gather(const orc_map* m, const pm_float3* pts, const float* brdf,
                int64_t nq, int32_t nthreads, pm_float3* out);
+int orc_gather_k(const orc_map* m, const pm_float3* pts, const float* brdf,
+                 int64_t nq, int32_t k, int32_t nthreads, pm_float3* out);
 int orc_camera_setup(pm_float3 look_from, pm_float3 look_at, pm_float3 look_up,
                      float fovy, int32_t w, int32_t h, pm_camera* out);
 /* Renders rows [row_lo, row_hi) of launch indices (pixelID.y); whole image if

@@ -37,7 +37,7 @@ hipError_t launch_map_export(const pm_photon_map* m, pm_kd_photon* out, hipStrea
 hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int k, float radius, int32_t* ids,
                       float* d2, float* maxd2, hipStream_t s);
 hipError_t launch_gather_api(const pm_photon_map* m, const pm_float3* pts, const float* brdf, int64_t nq,
-                             pm_float3* out, hipStream_t s);
+                             pm_float3* out, hipStream_t s, int k);
 hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int nl, pm_render_job* J,
                         hipStream_t s);
 hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba,
@@ -590,7 +590,17 @@ int pm_gather(const pm_photon_map* m, const pm_float3* pts, const float* brdf, i
   AllocStream alloc_scope(s);
   reset_phase(PH_GATHER);
   PhaseTimer tm(PH_GATHER, s);
-  return map_err(launch_gather_api(m, pts, brdf, nq, out, s));
+  return map_err(launch_gather_api(m, pts, brdf, nq, out, s, kKNearest));
+}
+
+int pm_gather_k(const pm_photon_map* m, const pm_float3* pts, const float* brdf, int64_t nq, int32_t k,
+                pm_float3* out, void* stream) {
+  if (!m || nq < 0 || k < 1 || k > 256 || (nq > 0 && (!pts || !brdf || !out))) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  reset_phase(PH_GATHER);
+  PhaseTimer tm(PH_GATHER, s);
+  return map_err(launch_gather_api(m, pts, brdf, nq, out, s, k));
 }
 
 int pm_camera_setup(pm_float3 from, pm_float3 at, pm_float3 up, float fovy, int32_t w, int32_t h, pm_camera* o) {
@@ -624,7 +634,8 @@ int pm_camera_setup(pm_float3 from, pm_float3 at, pm_float3 up, float fovy, int3
 
 static bool render_params_ok(const pm_scene* sc, const pm_render_params* P, const pm_light* lights, int32_t nl) {
   return sc && P && nl >= 0 && (nl == 0 || lights) && P->width > 0 && P->height > 0 && P->samples_per_pixel > 0 &&
-         P->max_depth >= 0 && !(P->tile_count > 1 && (P->tile_rank < 0 || P->tile_rank >= P->tile_count));
+         P->max_depth >= 0 && !(P->tile_count > 1 && (P->tile_rank < 0 || P->tile_rank >= P->tile_count)) &&
+         P->caustic_k >= 0 && P->caustic_k <= 256;
 }
 
 int pm_render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int32_t nl, pm_render_job** out,

@@ -339,16 +339,22 @@ __device__ __forceinline__ float radiance_r2(const double (&list)[K], float r2) 
 
 // pm_knn: K-wide list for k <= K; k > 128 runs 128-wide passes (j0 = output
 // offset of this pass, lo_in / lo_out = last key of the previous / this pass).
-template <int K, int QP>
+// QL > 0: candidates go through a QL-deep per-lane LDS queue (knn_walk), as in
+// the gather; the 128-wide passes of k > 128 use it (config 5, k = 200).
+template <int K, int QP, int QL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 64 ? 4 : 1))) void k_knn(
     const float4* nodes, int n, const pm_float3* q, int64_t nq, int k, int j0, float r2, int32_t* ids, float* d2o,
     float* maxd2, const double* lo_in, double* lo_out) {
+  __shared__ double lq[QL > 0 ? QL * 256 : 1];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < nq;
   double list[K];
   const pm_float3 p = valid ? q[i] : pm_float3{0.f, 0.f, 0.f};
   const double lo = (valid && lo_in) ? lo_in[i] : 0.0;
-  knn_walk<K, true, QP, false>(nodes, n, mk(p), r2, valid, list, nullptr, nullptr, 0, lo);
+  // a previous pass whose list did not fill (last key = the sentinel, id -1)
+  // found every candidate: this pass has none to find, its walk is skipped
+  const bool done = lo_in && key_id(lo) == 0xFFFFFFFFu;
+  knn_walk<K, true, QP, false, QL>(nodes, n, mk(p), r2, valid && !done, list, nullptr, lq + threadIdx.x, 256, lo);
   if (!valid) return;
 #pragma unroll
   for (int j = 0; j < K; j++) {
@@ -709,14 +715,29 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
   PM_KNN_CASE(128, 0)
 #undef PM_KNN_CASE
   if (k > 256) return hipErrorInvalidValue;
-  // 128 < k <= 256: two exact 128-wide passes
-  DevBuf<double> lo(nq);
-  if (!lo.p) return hipErrorOutOfMemory;
-  k_knn<128, 0><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, 0, r2, ids, d2, maxd2, nullptr, lo.p);
-  PM_HIP_TRY(hipGetLastError());
-  k_knn<128, 0><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, 128, r2, ids, d2, maxd2, lo.p, nullptr);
-  PM_HIP_TRY(hipGetLastError());
-  return hipStreamSynchronize(s);   // lo is freed on return
+  // 128 < k <= 256: exact passes of W keys, each collecting the W smallest keys
+  // above the previous pass's last (PM_KNN_PASS_W: 128 (2 passes, 256 VGPRs,
+  // 2 waves/SIMD) or 64 (4 passes, 128 VGPRs, 4 waves/SIMD))
+  const char* wenv = std::getenv("PM_KNN_PASS_W");
+  const int W = (wenv && std::atoi(wenv) == 64) ? 64 : 128;
+  const char* qenv = std::getenv("PM_KNN_QUEUE");   // LDS insert queue in the 128-wide passes
+  const bool ql = !qenv || std::atoi(qenv) != 0;
+  DevBuf<double> la(nq), lb(nq);
+  if (!la.p || !lb.p) return hipErrorOutOfMemory;
+  double *lin = nullptr, *lout = la.p;
+  for (int j0 = 0; j0 < k; j0 += W) {
+    double* lo_out = j0 + W < k ? lout : nullptr;
+    if (W == 64)
+      k_knn<64, 0><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, j0, r2, ids, d2, maxd2, lin, lo_out);
+    else if (ql)
+      k_knn<128, 0, 8><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, j0, r2, ids, d2, maxd2, lin, lo_out);
+    else
+      k_knn<128, 0><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, j0, r2, ids, d2, maxd2, lin, lo_out);
+    PM_HIP_TRY(hipGetLastError());
+    lin = lout;
+    lout = lout == la.p ? lb.p : la.p;
+  }
+  return hipStreamSynchronize(s);   // the pass bounds are freed on return
 }
 
 hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,
@@ -796,14 +817,66 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   return hipGetLastError();
 }
 
+// ---- radiance estimate with k != 50 neighbours (k = 200
+// caustic gather). gatherPhotons (shading.h:93-121) over the k nearest: the
+// exact lists come from the pm_knn passes (k <= 128 one pass, up to 256 in
+// 128-wide passes), then one kernel sums them in (d^2, index) order with
+// r^2 = the k-th d^2 (max_radius^2 if fewer were found), as for k = 50.
+__global__ void k_q3_from_dense(const float4* __restrict__ qb, const uint32_t* __restrict__ perm, int64_t nq,
+                                pm_float3* __restrict__ q3) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  const float4 q = qb[perm ? (int64_t)perm[i] : i];
+  q3[i] = {q.x, q.y, q.z};
+}
+
+__global__ void k_radiance_k(const float4* __restrict__ qb, const uint32_t* __restrict__ perm, int64_t nq, int k,
+                             const int32_t* __restrict__ ids, const float* __restrict__ d2,
+                             const float* __restrict__ maxd2, const float4* __restrict__ payload,
+                             float4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  const int64_t r = perm ? (int64_t)perm[i] : i;
+  const float brdf = qb[r].w;
+  const float r2 = maxd2[i];
+  v3 flux = {0.f, 0.f, 0.f};
+  for (int j = 0; j < k; j++) {
+    const int32_t id = ids[i * k + j];
+    if (id < 0) continue;
+    const float4 pl = payload[id];
+    const float dist = sqrtf(d2[i * k + j]);
+    const float w = 1 - (dist / sqrtf(r2) * kConeFilterC);
+    flux = add(flux, smul(brdf * pl.w * w, v3{pl.x, pl.y, pl.z}));
+  }
+  const v3 f = divf(flux, (1 - (2.f / 3.f) * (1.f / kConeFilterC)) * 2 * kPI * r2);
+  out[r] = make_float4(f.x, f.y, f.z, 0.f);
+}
+
+hipError_t launch_gather_k(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,
+                           int k, const uint32_t* perm) {
+  if (nq <= 0) return hipSuccess;
+  if (k < 1 || k > 256) return hipErrorInvalidValue;
+  if (k == kKNearest) return launch_gather(m, qb, nq, out, s, 0, perm);
+  DevBuf<pm_float3> q3(nq);
+  DevBuf<int32_t> ids((size_t)nq * k);
+  DevBuf<float> d2((size_t)nq * k), md(nq);
+  if (!q3.p || !ids.p || !d2.p || !md.p) return hipErrorOutOfMemory;
+  k_q3_from_dense<<<grid_for(nq, 256), 256, 0, s>>>(qb, perm, nq, q3.p);
+  PM_HIP_TRY(hipGetLastError());
+  PM_HIP_TRY(launch_knn(m, q3.p, nq, k, kKMaxDistance, ids.p, d2.p, md.p, s));
+  k_radiance_k<<<grid_for(nq, 256), 256, 0, s>>>(qb, perm, nq, k, ids.p, d2.p, md.p, m->payload.p, out);
+  PM_HIP_TRY(hipGetLastError());
+  return hipStreamSynchronize(s);   // the lists are freed on return
+}
+
 hipError_t launch_gather_api(const pm_photon_map* m, const pm_float3* pts, const float* brdf, int64_t nq,
-                             pm_float3* out, hipStream_t s) {
+                             pm_float3* out, hipStream_t s, int k) {
   if (nq <= 0) return hipSuccess;
   DevBuf<float4> qb(nq), ob(nq);
   if (!qb.p || !ob.p) return hipErrorOutOfMemory;
   k_pack_query<<<grid_for(nq, 256), 256, 0, s>>>(pts, brdf, nq, qb.p);
   PM_HIP_TRY(hipGetLastError());
-  PM_HIP_TRY(launch_gather(m, qb.p, nq, ob.p, s));
+  PM_HIP_TRY(launch_gather_k(m, qb.p, nq, ob.p, s, k, nullptr));
   k_unpack_out<<<grid_for(nq, 256), 256, 0, s>>>(ob.p, nq, out);
   PM_HIP_TRY(hipGetLastError());
   return hipStreamSynchronize(s);

@@ -79,6 +79,10 @@ hipError_t kd_shard_assemble(const float4* elems, const float4* top, int L, cons
 hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
                                      float pb, float4* elems, float4* payload, hipStream_t s);
 
+// gatherPhotons over k != 50 neighbours (pm_knn passes + one summing kernel).
+hipError_t launch_gather_k(const pm_photon_map* m, const float4* d_query, int64_t nq, float4* d_out, hipStream_t s,
+                           int k, const uint32_t* perm);
+
 // K = 50 gather (gatherPhotons) for a batch of queries.
 // tag 0: API / caustic-map launches, 1: global-map launch (separate kernel symbol for rocprof)
 hipError_t launch_gather(const pm_photon_map* m, const float4* d_query /*pos, brdf*/, int64_t nq,

@@ -38,6 +38,7 @@ struct LightR {
 
 struct RenderArgs {
   int32_t W, H, spp, depth;
+  int32_t caustic_k;   // host side only: neighbours of the caustic gather
   int32_t tile_rank, tile_count, tiles_x, my_tiles;
   v3 cam_pos, d00, du, dv, sky;
   const LightR* lights;
@@ -454,12 +455,14 @@ static hipError_t sort_queries(const float4* dense, int64_t n, const pm_box& bb,
   return radix_sort_pairs(Q.keys.p, Q.perm.p, n, 30, s);
 }
 
-static hipError_t gather_sorted(const pm_photon_map* m, SortedQueries& Q, float4* res, int tag, hipStream_t s) {
+static hipError_t gather_sorted(const pm_photon_map* m, SortedQueries& Q, float4* res, int tag, hipStream_t s,
+                                int k = kKNearest) {
   if (Q.n <= 0) return hipSuccess;
   {
     PhaseTimer tg(tag == 1 ? PH_GATHER_GLOBAL : PH_COUNT, s);
     // lanes take the queries in Morton order and write each result in place
-    PM_HIP_TRY(launch_gather(m, Q.dense, Q.n, res, s, tag, Q.perm.p));
+    if (k == kKNearest) PM_HIP_TRY(launch_gather(m, Q.dense, Q.n, res, s, tag, Q.perm.p));
+    else PM_HIP_TRY(launch_gather_k(m, Q.dense, Q.n, res, s, k, Q.perm.p));
   }
   return hipSuccess;
 }
@@ -580,6 +583,7 @@ hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light*
   A.H = P->height;
   A.spp = P->samples_per_pixel;
   A.depth = P->max_depth;
+  A.caustic_k = P->caustic_k > 0 ? P->caustic_k : kKNearest;
   A.tile_rank = P->tile_count > 1 ? P->tile_rank : 0;
   A.tile_count = P->tile_count > 1 ? P->tile_count : 1;
   A.tiles_x = (A.W + 15) / 16;
@@ -727,7 +731,7 @@ hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_p
   if (J->nthreads == 0) return hipSuccess;
   {
     PhaseTimer tm(PH_GATHER, s);
-    PM_HIP_TRY(gather_sorted(cmap, J->cs, J->cres.p, 0, s));
+    PM_HIP_TRY(gather_sorted(cmap, J->cs, J->cres.p, 0, s, J->A.caustic_k));
     PM_HIP_TRY(gather_sorted(gmap, J->gs, J->gres.p, 1, s));
   }
   PathOut O{J->vdirect.p, J->vatt.p, J->valb.p, J->vflags.p, J->cq.p, J->cvalid.p, J->gq.p, J->galb.p,

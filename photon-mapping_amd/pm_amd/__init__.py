@@ -103,7 +103,7 @@ class TraceParams(C.Structure):
 class RenderParams(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("samples_per_pixel", C.c_int32),
                 ("max_depth", C.c_int32), ("camera", Camera), ("sky_colour", Float3),
-                ("tile_rank", C.c_int32), ("tile_count", C.c_int32)]
+                ("tile_rank", C.c_int32), ("tile_count", C.c_int32), ("caustic_k", C.c_int32)]
 
 
 class RenderStats(C.Structure):
@@ -164,6 +164,7 @@ _SIGNATURES = {
     "pm_kd_shard_plan_destroy": (C.c_int, [_P]),
     "pm_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_float, _P, _P, _P, _P]),
     "pm_gather": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P]),
+    "pm_gather_k": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, _P, _P]),
     "pm_camera_setup": (C.c_int, [Float3, Float3, Float3, C.c_float, C.c_int32, C.c_int32, C.POINTER(Camera)]),
     "pm_render": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Light), C.c_int32, _P, _P, _P, _P, _P]),
     "pm_render_stats_get": (C.c_int, [C.POINTER(RenderStats)]),
@@ -556,12 +557,17 @@ def knn(pmap: PhotonMap, queries, k: int = 50, max_radius: float = 100.0, stream
     return ids, d2, md
 
 
-def gather_photons(pmap: PhotonMap, points, brdf, stream=None):
-    """gatherPhotons (shading.h:93-121) for a batch of hit points."""
+def gather_photons(pmap: PhotonMap, points, brdf, stream=None, k: int = 50):
+    """gatherPhotons (shading.h:93-121) for a batch of hit points; k != 50
+    (up to 256) is pm_gather_k (config 5's k = 200 caustic gather)."""
     import torch
     nq = points.shape[0]
     out = torch.empty((nq, 3), dtype=torch.float32, device="cuda")
-    _check(_lib.pm_gather(pmap.handle, _ptr(points), _ptr(brdf), nq, _ptr(out), _stream(stream)), "pm_gather")
+    if k == 50:
+        _check(_lib.pm_gather(pmap.handle, _ptr(points), _ptr(brdf), nq, _ptr(out), _stream(stream)), "pm_gather")
+    else:
+        _check(_lib.pm_gather_k(pmap.handle, _ptr(points), _ptr(brdf), nq, int(k), _ptr(out), _stream(stream)),
+               "pm_gather_k")
     return out
 
 
@@ -575,12 +581,13 @@ def setup_camera(look_from, look_at, look_up, fovy, width, height) -> Camera:
 
 def render(scene: Scene, camera: Camera, width: int, height: int, spp: int, depth: int, sky, lights,
            global_map: PhotonMap, caustic_map: PhotonMap, tile_rank: int = 0, tile_count: int = 1,
-           want_rgb: bool = True, rgba=None, stream=None):
+           want_rgb: bool = True, rgba=None, stream=None, caustic_k: int = 0):
     """owlRayGenLaunch2D(simpleRayGen, W, H) (ray-tracer/src/hostCode.cu:231-237).
+    caustic_k: neighbours of the caustic gather (0 = the reference's 50; config 5: 200).
     Returns (rgba int32 [H,W], rgb float32 [H,W,3] or None)."""
     import torch
     p = RenderParams(int(width), int(height), int(spp), int(depth), camera, _f3(sky), int(tile_rank),
-                     int(tile_count))
+                     int(tile_count), int(caustic_k))
     la = lights_array(lights)
     if rgba is None:
         rgba = torch.zeros((height, width), dtype=torch.int32, device="cuda")
@@ -598,11 +605,11 @@ class RenderJob:
     the gathers and resolve. begin + finish == render()."""
 
     def __init__(self, scene: Scene, camera: Camera, width: int, height: int, spp: int, depth: int, sky, lights,
-                 tile_rank: int = 0, tile_count: int = 1, stream=None):
+                 tile_rank: int = 0, tile_count: int = 1, stream=None, caustic_k: int = 0):
         self.width, self.height = int(width), int(height)
         self._scene = scene   # keeps the scene alive while the job refers to it
         p = RenderParams(self.width, self.height, int(spp), int(depth), camera, _f3(sky), int(tile_rank),
-                         int(tile_count))
+                         int(tile_count), int(caustic_k))
         la = lights_array(lights)
         h = _P()
         _check(_lib.pm_render_begin(scene.handle, C.byref(p), la, len(lights), C.byref(h), _stream(stream)),

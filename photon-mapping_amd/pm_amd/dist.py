@@ -44,6 +44,8 @@ class FrameConfig:
     quantize: bool = False
     # split the global map's kd-tree build across ranks (N > 1; identical tree)
     shard_build: bool = True
+    # neighbours of the caustic gather (0: the reference's 50; config 5: 200)
+    caustic_k: int = 0
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -192,7 +194,7 @@ class GpuBackend:
         pm = self.pm
         c = self.cfg
         pm.render(self.scene, self.cam, c.width, c.height, c.spp, c.depth, c.sky, self.lights, gm, cm,
-                  tile_rank=tile_rank, tile_count=tile_count, want_rgb=False, rgba=rgba)
+                  tile_rank=tile_rank, tile_count=tile_count, want_rgb=False, rgba=rgba, caustic_k=c.caustic_k)
         for k in ("paths", "gather", "gather_global", "resolve"):
             self.phase[k] = pm.phase_us(k)
         return rgba

@@ -187,6 +187,16 @@ def sponza_class() -> Tuple[List[MeshData], List[dict]]:
     return meshes, lights
 
 
+def sponza_caustics() -> Tuple[List[MeshData], List[dict]]:
+    """the same atrium (glass and mirror spheres on plinths)
+    lit by one SQUARE_LIGHT (this build's area-light emission, pm.h) under the
+    roof, facing down."""
+    meshes, _ = sponza_class()
+    lights = [{"pos": (0.0, 38.0, 0.0), "rgb": (1.0, 0.97, 0.92), "power": 2000.0,
+               "normal": (0.0, -1.0, 0.0), "side": 12.0}]
+    return meshes, lights
+
+
 def scene_summary(meshes) -> dict:
     return {"meshes": len(meshes), "triangles": int(sum(len(m.indices) for m in meshes)),
             "vertices": int(sum(len(m.vertices) for m in meshes))}

@@ -61,7 +61,7 @@ def test_status_strings():
     import pm_amd
     for s in range(8):
         assert pm_amd.lib.pm_status_string(s)
-    assert pm_amd.lib.pm_abi_version() == 1
+    assert pm_amd.lib.pm_abi_version() == 2   # 2: pm_render_params.caustic_k
 
 
 def test_no_cpu_fallback_without_gpu(cornell):

@@ -291,7 +291,7 @@ def test_photon_map_export(cornell):
     assert np.all(e[:, 9] == 1.0)
 
 
-def _render_pair(meshes, lights, casted, W, H, spp, tiles=(0, 1)):
+def _render_pair(meshes, lights, casted, W, H, spp, tiles=(0, 1), caustic_k=0):
     import oracle
     import pm_amd
     os_ = oracle.Scene(meshes)
@@ -304,11 +304,11 @@ def _render_pair(meshes, lights, casted, W, H, spp, tiles=(0, 1)):
     ocam = oracle.camera_setup((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
     assert bytes(cam) == bytes(ocam)
     rgba, rgb = pm_amd.render(gs, cam, W, H, spp, 30, (1, 1, 1), lights, gmap, cmap, tile_rank=tiles[0],
-                              tile_count=tiles[1])
+                              tile_count=tiles[1], caustic_k=caustic_k)
     om_g = oracle.PhotonMap(g_np, 1.0, c_np, 0.5)
     om_c = oracle.PhotonMap(c_np, 0.5)
     orgba, orgb, ost = oracle.render(os_, ocam, W, H, spp, 30, (1, 1, 1), lights, om_g, om_c,
-                                     tile_rank=tiles[0], tile_count=tiles[1])
+                                     tile_rank=tiles[0], tile_count=tiles[1], caustic_k=caustic_k)
     return rgba.cpu().numpy().view(np.uint32), rgb.cpu().numpy(), orgba, orgb, ost
 
 
@@ -587,3 +587,38 @@ def test_trace_sort_knob_bitwise(cornell, monkeypatch):
     got = [pm_amd.run_point_light_ray_gen(gs, lights, 50000, 10, m) for m in (False, True)]
     for a, b in zip(ref, got):
         assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+@pytest.mark.parametrize("k", [1, 8, 50, 64, 128, 129, 200, 256])
+def test_gather_k_vs_oracle(cornell, k):
+    """pm_gather_k (config 5: k = 200 caustic gather): the radiance estimate over
+    the k nearest equals the oracle's bit for bit, incl. lists that do not fill."""
+    import oracle
+    import pm_amd
+    meshes, lights = cornell
+    os_ = oracle.Scene(meshes)
+    g = oracle.trace(os_, lights, 20000, 10, False)
+    c = oracle.trace(os_, lights, 20000, 10, True)
+    rng = np.random.default_rng(9)
+    q = np.concatenate([g[rng.integers(0, len(g), 1500), 0:3] + rng.normal(scale=0.5, size=(1500, 3)),
+                        rng.uniform(-300, 300, size=(100, 3))]).astype(np.float32)   # + far queries
+    brdf = rng.uniform(0, 0.4, size=len(q)).astype(np.float32)
+    for a, pa, b, pb in ((g, 1.0, c, 0.5), (c, 0.5, None, 0.0)):
+        gm = pm_amd.PhotonMap(torch.from_numpy(a).cuda(), pa, None if b is None else torch.from_numpy(b).cuda(), pb)
+        om = oracle.PhotonMap(a, pa, b, pb)
+        fg = pm_amd.gather_photons(gm, torch.from_numpy(q).cuda(), torch.from_numpy(brdf).cuda(), k=k).cpu().numpy()
+        assert np.array_equal(_bits(fg), _bits(om.gather(q, brdf, k=k)))
+
+
+def test_render_caustic_k200_vs_oracle(cornell):
+    """Config 5's caustic gather (k = 200) inside pm_render matches the oracle's
+    render with the same k; k = 0 and k = 50 are the reference render."""
+    import pm_amd
+    meshes, lights = cornell
+    rgba, rgb, orgba, orgb, _ = _render_pair(meshes, lights, 20000, 48, 36, 1, caustic_k=200)
+    assert np.abs(np.clip(rgb, 0, 1) - np.clip(orgb, 0, 1)).max() <= 1e-3
+    assert np.mean(_bits(rgb) == _bits(orgb)) >= 0.999
+    ref = _render_pair(meshes, lights, 20000, 48, 36, 1)[1]
+    k50 = _render_pair(meshes, lights, 20000, 48, 36, 1, caustic_k=50)[1]
+    assert np.array_equal(_bits(ref), _bits(k50))
+    assert not np.array_equal(_bits(ref), _bits(rgb))   # 200 neighbours change the caustic term
