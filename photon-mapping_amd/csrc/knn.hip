@@ -344,7 +344,7 @@ __device__ __forceinline__ float radiance_r2(const double (&list)[K], float r2) 
 template <int K, int QP, int QL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 64 ? 4 : 1))) void k_knn(
     const float4* nodes, int n, const pm_float3* q, int64_t nq, int k, int j0, float r2, int32_t* ids, float* d2o,
-    float* maxd2, const double* lo_in, double* lo_out) {
+    float* maxd2, const double* lo_in, double* lo_out, const float* cutq = nullptr) {
   __shared__ double lq[QL > 0 ? QL * 256 : 1];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < nq;
@@ -354,17 +354,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 64 ? 4
   // a previous pass whose list did not fill (last key = the sentinel, id -1)
   // found every candidate: this pass has none to find, its walk is skipped
   const bool done = lo_in && key_id(lo) == 0xFFFFFFFFu;
-  knn_walk<K, true, QP, false, QL>(nodes, n, mk(p), r2, valid && !done, list, nullptr, lq + threadIdx.x, 256, lo);
+  // cutq: a seeded (strict) cut-off per query, <= r2, that provably admits the
+  // pass's keys (launch_gather_k); the reported radius stays r2
+  const float rw = (valid && cutq) ? cutq[i] : r2;
+  knn_walk<K, true, QP, false, QL>(nodes, n, mk(p), rw, valid && !done, list, nullptr, lq + threadIdx.x, 256, lo);
   if (!valid) return;
 #pragma unroll
   for (int j = 0; j < K; j++) {
     const int jj = j0 + j;
+    const bool empty = key_id(list[j]) == 0xFFFFFFFFu;
     if (jj < k) {
-      const uint32_t id = key_id(list[j]);
-      ids[i * k + jj] = id == 0xFFFFFFFFu ? -1 : (int32_t)id;
-      if (d2o) d2o[i * k + jj] = key_d2(list[j]);
+      ids[i * k + jj] = empty ? -1 : (int32_t)key_id(list[j]);
+      if (d2o) d2o[i * k + jj] = empty ? r2 : key_d2(list[j]);
     }
-    if (jj == k - 1 && maxd2) maxd2[i] = key_d2(list[j]);
+    if (jj == k - 1 && maxd2) maxd2[i] = empty ? r2 : key_d2(list[j]);
   }
   if (lo_out) lo_out[i] = list[K - 1];
 }
@@ -696,16 +699,17 @@ static std::vector<int64_t> seed_levels() {
   return v;
 }
 
+// cut1 / cut2 (optional): per-query strict cut-offs of the first / second pass
 hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int k, float radius, int32_t* ids,
-                      float* d2, float* maxd2, hipStream_t s) {
+                      float* d2, float* maxd2, hipStream_t s, const float* cut1, const float* cut2) {
   if (nq <= 0) return hipSuccess;
   const float r2 = radius * radius;
   const int n = (int)m->n;
   const int g = grid_for(nq, 256);
-#define PM_KNN_CASE(KK, QQ)                                                                        \
-  if (k <= KK) {                                                                                   \
-    k_knn<KK, QQ><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, 0, r2, ids, d2, maxd2, nullptr, nullptr); \
-    return hipGetLastError();                                                                      \
+#define PM_KNN_CASE(KK, QQ)                                                                                \
+  if (k <= KK) {                                                                                           \
+    k_knn<KK, QQ><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, 0, r2, ids, d2, maxd2, nullptr, nullptr, cut1); \
+    return hipGetLastError();                                                                              \
   }
   PM_KNN_CASE(8, 0)
   PM_KNN_CASE(16, 0)
@@ -727,12 +731,13 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
   double *lin = nullptr, *lout = la.p;
   for (int j0 = 0; j0 < k; j0 += W) {
     double* lo_out = j0 + W < k ? lout : nullptr;
+    const float* cut = (W == 128) ? (j0 == 0 ? cut1 : cut2) : nullptr;
     if (W == 64)
       k_knn<64, 0><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, j0, r2, ids, d2, maxd2, lin, lo_out);
     else if (ql)
-      k_knn<128, 0, 8><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, j0, r2, ids, d2, maxd2, lin, lo_out);
+      k_knn<128, 0, 8><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, j0, r2, ids, d2, maxd2, lin, lo_out, cut);
     else
-      k_knn<128, 0><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, j0, r2, ids, d2, maxd2, lin, lo_out);
+      k_knn<128, 0><<<g, 256, 0, s>>>(m->nodes.p, n, q, nq, k, j0, r2, ids, d2, maxd2, lin, lo_out, cut);
     PM_HIP_TRY(hipGetLastError());
     lin = lout;
     lout = lout == la.p ? lb.p : la.p;
@@ -852,6 +857,37 @@ __global__ void k_radiance_k(const float4* __restrict__ qb, const uint32_t* __re
   out[r] = make_float4(f.x, f.y, f.z, 0.f);
 }
 
+// Seeded cut-offs for the general-k passes (the same triangle-inequality bound
+// as k_gather_level): every 16th query in walk order is a leader and runs the
+// plain passes first; a query's pass-1 cut comes from the leaders' min(k, 128)-th
+// d^2, its pass-2 cut from their k-th d^2 (a leader whose list did not fill
+// seeds nothing). Strict cut-offs (k_knn admits d^2 < cut).
+__global__ void k_q3_leaders(const pm_float3* __restrict__ q3, int64_t nl, pm_float3* __restrict__ q3l) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < nl) q3l[j] = q3[j * kSeedStride];
+}
+__global__ void k_knn_cuts(const pm_float3* __restrict__ q3, int64_t nq, const pm_float3* __restrict__ q3l,
+                           int64_t nl, int k, const int32_t* __restrict__ idsl, const float* __restrict__ d2l,
+                           float* __restrict__ cut1, float* __restrict__ cut2) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nq) return;
+  const v3 q = {q3[r].x, q3[r].y, q3[r].z};
+  const float R2 = kKMaxDistance * kKMaxDistance;
+  const int k1 = k < 128 ? k : 128;
+  const int64_t jp = r / kSeedStride;
+  double b1 = 1e300, b2 = 1e300;
+  for (int64_t j = jp - 1; j <= jp + 2; j++) {
+    if (j < 0 || j >= nl) continue;
+    const float4 p = make_float4(q3l[j].x, q3l[j].y, q3l[j].z, 0.f);
+    const int64_t a = j * k + (k1 - 1), c = j * k + (k - 1);
+    b1 = fmin(b1, seed_bound(make_float4(p.x, p.y, p.z, idsl[a] >= 0 ? d2l[a] : -1.f), q));
+    b2 = fmin(b2, seed_bound(make_float4(p.x, p.y, p.z, idsl[c] >= 0 ? d2l[c] : -1.f), q));
+  }
+  // seed_cut is inclusive (d^2 <= cut); the next float up makes it strict
+  cut1[r] = __uint_as_float(__float_as_uint(seed_cut(b1, R2)) + 1u);
+  cut2[r] = __uint_as_float(__float_as_uint(seed_cut(b2, R2)) + 1u);
+}
+
 hipError_t launch_gather_k(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,
                            int k, const uint32_t* perm) {
   if (nq <= 0) return hipSuccess;
@@ -863,7 +899,26 @@ hipError_t launch_gather_k(const pm_photon_map* m, const float4* qb, int64_t nq,
   if (!q3.p || !ids.p || !d2.p || !md.p) return hipErrorOutOfMemory;
   k_q3_from_dense<<<grid_for(nq, 256), 256, 0, s>>>(qb, perm, nq, q3.p);
   PM_HIP_TRY(hipGetLastError());
-  PM_HIP_TRY(launch_knn(m, q3.p, nq, k, kKMaxDistance, ids.p, d2.p, md.p, s));
+  // PM_KNN_SEED=1: leader-seeded cut-offs (bitwise the same). Config 5 measured
+  // slower (caustic gather 195 -> 240 ms): the 128-wide passes are bound by their
+  // >= 128 inserts of 255 ops each, which a tighter cut does not remove.
+  const char* senv = std::getenv("PM_KNN_SEED");
+  if (senv && std::atoi(senv) != 0 && nq > kSeedStride && m->n > 0) {
+    const int64_t nl = (nq + kSeedStride - 1) / kSeedStride;
+    DevBuf<pm_float3> q3l(nl);
+    DevBuf<int32_t> idsl((size_t)nl * k);
+    DevBuf<float> d2l((size_t)nl * k), mdl(nl), c1(nq), c2(nq);
+    if (!q3l.p || !idsl.p || !d2l.p || !mdl.p || !c1.p || !c2.p) return hipErrorOutOfMemory;
+    k_q3_leaders<<<grid_for(nl, 256), 256, 0, s>>>(q3.p, nl, q3l.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(launch_knn(m, q3l.p, nl, k, kKMaxDistance, idsl.p, d2l.p, mdl.p, s, nullptr, nullptr));
+    k_knn_cuts<<<grid_for(nq, 256), 256, 0, s>>>(q3.p, nq, q3l.p, nl, k, idsl.p, d2l.p, c1.p, c2.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(launch_knn(m, q3.p, nq, k, kKMaxDistance, ids.p, d2.p, md.p, s, c1.p, c2.p));
+    PM_HIP_TRY(hipStreamSynchronize(s));   // leader buffers are freed on return
+  } else {
+    PM_HIP_TRY(launch_knn(m, q3.p, nq, k, kKMaxDistance, ids.p, d2.p, md.p, s, nullptr, nullptr));
+  }
   k_radiance_k<<<grid_for(nq, 256), 256, 0, s>>>(qb, perm, nq, k, ids.p, d2.p, md.p, m->payload.p, out);
   PM_HIP_TRY(hipGetLastError());
   return hipStreamSynchronize(s);   // the lists are freed on return

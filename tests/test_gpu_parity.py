@@ -589,8 +589,9 @@ def test_trace_sort_knob_bitwise(cornell, monkeypatch):
         assert torch.equal(a.view(torch.int32), b.view(torch.int32))
 
 
+@pytest.mark.parametrize("seed", ["1", "0"])
 @pytest.mark.parametrize("k", [1, 8, 50, 64, 128, 129, 200, 256])
-def test_gather_k_vs_oracle(cornell, k):
+def test_gather_k_vs_oracle(cornell, k, seed, monkeypatch):
     """pm_gather_k (config 5: k = 200 caustic gather): the radiance estimate over
     the k nearest equals the oracle's bit for bit, incl. lists that do not fill."""
     import oracle
@@ -603,6 +604,8 @@ def test_gather_k_vs_oracle(cornell, k):
     q = np.concatenate([g[rng.integers(0, len(g), 1500), 0:3] + rng.normal(scale=0.5, size=(1500, 3)),
                         rng.uniform(-300, 300, size=(100, 3))]).astype(np.float32)   # + far queries
     brdf = rng.uniform(0, 0.4, size=len(q)).astype(np.float32)
+    q = q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))]   # spatial order: tight leader seeds (PM_KNN_SEED)
+    monkeypatch.setenv("PM_KNN_SEED", seed)
     for a, pa, b, pb in ((g, 1.0, c, 0.5), (c, 0.5, None, 0.0)):
         gm = pm_amd.PhotonMap(torch.from_numpy(a).cuda(), pa, None if b is None else torch.from_numpy(b).cuda(), pb)
         om = oracle.PhotonMap(a, pa, b, pb)
