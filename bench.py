@@ -117,11 +117,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus or (world == 1 and args.gpus == 1), f"--gpus {args.gpus} but WORLD_SIZE={world}"
-    torch.cuda.set_device(local_rank)
+    # PM_DIST_BACKEND=gloo: every rank on cuda:0 with host-staged collectives, to
+    # exercise the N > 1 path on a one-GPU box (the scaling runs use RCCL)
+    backend_name = os.environ.get("PM_DIST_BACKEND", "nccl")
+    torch.cuda.set_device(0 if backend_name == "gloo" else local_rank)
     dist = None
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        import torch.distributed as tdist
+        if backend_name == "gloo":
+            tdist.init_process_group("gloo")
+            dist = pmdist.HostStagedDist(tdist)
+        else:
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist = tdist
 
     if args.scene == "sponza" and args.config == 5:
         meshes, lights = scenes.sponza_caustics()

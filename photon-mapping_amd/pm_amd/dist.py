@@ -73,6 +73,44 @@ def allgather_rows(t, world: int, dist):
     return torch.cat(parts)
 
 
+class HostStagedDist:
+    """torch.distributed over gloo with CUDA tensors staged through host memory:
+    lets several ranks share one GPU (tests, and `bench.py` with
+    PM_DIST_BACKEND=gloo on a one-GPU box); production runs use RCCL directly."""
+
+    def __init__(self, dist):
+        import torch
+        self.d, self.t = dist, torch
+        self.ReduceOp = dist.ReduceOp
+
+    def all_gather(self, outs, t):
+        hs = [self.t.empty_like(o, device="cpu") for o in outs]
+        self.d.all_gather(hs, t.cpu())
+        for o, h in zip(outs, hs):
+            o.copy_(h)
+
+    def all_gather_into_tensor(self, out, t):
+        h = self.t.empty_like(out, device="cpu")
+        self.d.all_gather_into_tensor(h, t.cpu())
+        out.copy_(h)
+
+    def reduce(self, t, dst, op):
+        h = t.cpu()
+        self.d.reduce(h, dst=dst, op=op)
+        t.copy_(h)
+
+    def all_reduce(self, t, op):
+        h = t.cpu()
+        self.d.all_reduce(h, op=op)
+        t.copy_(h)
+
+    def barrier(self):
+        self.d.barrier()
+
+    def destroy_process_group(self):
+        self.d.destroy_process_group()
+
+
 def pack_rows(t):
     """pm_photon rows (n, 10) -> (n, 6): position, colour."""
     import torch

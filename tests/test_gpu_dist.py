@@ -18,30 +18,6 @@ torch = pytest.importorskip("torch")
 W, H = 64, 48
 
 
-class StagedDist:
-    """torch.distributed over gloo with CUDA tensors staged through host memory."""
-
-    def __init__(self, dist):
-        self.d = dist
-        self.ReduceOp = dist.ReduceOp
-
-    def all_gather(self, outs, t):
-        hs = [torch.empty_like(o, device="cpu") for o in outs]
-        self.d.all_gather(hs, t.cpu())
-        for o, h in zip(outs, hs):
-            o.copy_(h)
-
-    def all_gather_into_tensor(self, out, t):
-        h = torch.empty_like(out, device="cpu")
-        self.d.all_gather_into_tensor(h, t.cpu())
-        out.copy_(h)
-
-    def reduce(self, t, dst, op):
-        h = t.cpu()
-        self.d.reduce(h, dst=dst, op=op)
-        t.copy_(h)
-
-
 def _frame(rank, world, dist):
     import pm_amd
     from pm_amd import dist as pmdist
@@ -59,7 +35,8 @@ def _worker(rank, world, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        img, ng = _frame(rank, world, StagedDist(dist))
+        from pm_amd.dist import HostStagedDist
+        img, ng = _frame(rank, world, HostStagedDist(dist))
         q.put((rank, img if rank == 0 else None, ng))
     finally:
         dist.destroy_process_group()
