@@ -110,3 +110,28 @@ def test_shard_ranges_partition():
             rs = [shard_range(total, r, world) for r in range(world)]
             assert rs[0][0] == 0 and rs[-1][1] == total
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+
+
+def test_shard_owners_balanced_and_deterministic():
+    """Subtree -> rank dealing of the split kd build (pm_amd.dist.shard_owners):
+    every subtree owned once, every rank used while subtrees last, the largest
+    rank load within one subtree of the mean, and the same answer every call."""
+    from pm_amd.dist import shard_owners
+    rng = np.random.default_rng(0)
+    for world in (2, 3, 4, 8, 16):
+        for _ in range(20):
+            sizes = [int(x) for x in rng.integers(1, 1000, size=2 * world)]
+            owner, load = shard_owners(sizes, world)
+            assert shard_owners(sizes, world) == (owner, load)
+            assert sorted(set(owner)) == list(range(world))
+            assert [sum(s for s, o in zip(sizes, owner) if o == r) for r in range(world)] == load
+            assert max(load) <= sum(sizes) / world + max(sizes)
+
+
+def test_pack_rows_round_trip():
+    """The exchange moves position + colour only (pack_rows / unpack_rows)."""
+    from pm_amd.dist import pack_rows, unpack_rows
+    t = torch.from_numpy(np.random.default_rng(1).normal(size=(37, 10)).astype(np.float32))
+    u = unpack_rows(pack_rows(t))
+    keep = [0, 1, 2, 7, 8, 9]
+    assert torch.equal(u[:, keep], t[:, keep]) and torch.count_nonzero(u[:, 3:7]) == 0
