@@ -295,6 +295,14 @@ __device__ __forceinline__ float box_area(const float b[6]) {
   return dx * dy + dy * dz + dz * dx;
 }
 
+// PM_BVH_PAIRS: binary node b with two triangle children stays a leaf; until
+// k_leaf_place lays the triangles out it is coded kPairCode - b
+constexpr int kPairCode = -(1 << 30);
+__device__ __forceinline__ bool is_pair(const float4* __restrict__ bin, int b) {
+  const int4 c = *reinterpret_cast<const int4*>(&bin[4 * b + 3]);
+  return c.x < 0 && c.y < 0;
+}
+
 __global__ void k_collapse_open(const float4* __restrict__ bin, const int2* __restrict__ frontier, int nf,
                                 float4* __restrict__ q, uint32_t* __restrict__ cnt) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
@@ -314,7 +322,7 @@ __global__ void k_collapse_open(const float4* __restrict__ bin, const int2* __re
     float barea = -1.0f;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-      if (c < m && code[c] >= 0) {
+      if (c < m && code[c] >= 0 && !(PM_BVH_PAIRS && is_pair(bin, code[c]))) {
         const float a = box_area(box[c]);
         if (a > barea) barea = a, best = c;
       }
@@ -341,6 +349,7 @@ __global__ void k_collapse_open(const float4* __restrict__ bin, const int2* __re
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     const bool used = c < m;
+    if (PM_BVH_PAIRS && used && code[c] >= 0 && is_pair(bin, code[c])) code[c] = kPairCode - code[c];
     if (used && code[c] >= 0) internal++;
 #pragma unroll
     for (int k = 0; k < 6; k++) qn[4 * k + c] = used ? box[c][k] : 0.0f;   // k: lo.x hi.x lo.y hi.y lo.z hi.z
@@ -503,6 +512,45 @@ __global__ void k_collapse_link8(const int2* __restrict__ frontier, int nf, cons
   }
 }
 
+// PM_BVH_PAIRS: triangles re-laid so that every leaf's triangles are contiguous
+// (node order), leaf codes ~(slot << 1 | count - 1)
+__device__ __forceinline__ int leaf_tris(int c) { return c == kBvhEmpty || c >= 0 ? 0 : (c <= kPairCode ? 2 : 1); }
+__global__ void k_leaf_count(const float4* __restrict__ q, int nn, uint32_t* __restrict__ cnt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nn) return;
+  const int4 c = *reinterpret_cast<const int4*>(&q[8 * (int64_t)i + 6]);
+  cnt[i] = leaf_tris(c.x) + leaf_tris(c.y) + leaf_tris(c.z) + leaf_tris(c.w);
+}
+__global__ void k_leaf_place(float4* __restrict__ q, int nn, const uint32_t* __restrict__ off,
+                             const float4* __restrict__ bin, const float4* __restrict__ tri,
+                             float4* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nn) return;
+  int4* cp = reinterpret_cast<int4*>(&q[8 * (int64_t)i + 6]);
+  int4 c4 = *cp;
+  int* cc = reinterpret_cast<int*>(&c4);
+  int next = (int)off[i];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int c = cc[k];
+    const int n = leaf_tris(c);
+    if (n == 0) continue;
+    int src[2];
+    if (n == 1) {
+      src[0] = ~c;
+    } else {
+      const int4 bc = *reinterpret_cast<const int4*>(&bin[4 * (kPairCode - c) + 3]);
+      src[0] = ~bc.x;
+      src[1] = ~bc.y;
+    }
+    for (int t = 0; t < n; t++)
+      for (int v = 0; v < 3; v++) out[3 * (int64_t)(next + t) + v] = tri[3 * (int64_t)src[t] + v];
+    cc[k] = ~((next << 1) | (n - 1));
+    next += n;
+  }
+  *cp = c4;
+}
+
 static hipError_t collapse_bvh(const float4* bin, int nbin, pm_scene* sc, hipStream_t s) {
   sc->nodes.alloc((size_t)8 * nbin);
   DevBuf<int2> fa(nbin), fb(nbin);
@@ -530,6 +578,23 @@ static hipError_t collapse_bvh(const float4* bin, int nbin, pm_scene* sc, hipStr
   }
   sc->nnodes = alloc;
   sc->depth = depth;
+  if (PM_BVH_PAIRS && kBvhWidth == 4) {
+    DevBuf<uint32_t> lc(alloc), lo(alloc), lt(1);
+    if (!lc.p || !lo.p || !lt.p) return hipErrorOutOfMemory;
+    k_leaf_count<<<grid_for(alloc, 256), 256, 0, s>>>(sc->nodes.p, alloc, lc.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(exclusive_scan_u32(lc.p, lo.p, alloc, lt.p, s));
+    uint32_t nt = 0;
+    PM_HIP_TRY(hipMemcpyAsync(&nt, lt.p, 4, hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    DevBuf<float4> laid((size_t)3 * nt);
+    if (!laid.p) return hipErrorOutOfMemory;
+    k_leaf_place<<<grid_for(alloc, 256), 256, 0, s>>>(sc->nodes.p, alloc, lo.p, bin, sc->tri.p, laid.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    std::swap(sc->tri.p, laid.p);
+    std::swap(sc->tri.n, laid.n);
+  }
   return hipSuccess;
 }
 

@@ -353,9 +353,28 @@ __device__ __forceinline__ bool leaf_hit(const float4 a, const float4 b, const f
   return false;
 }
 
+// PM_BVH_PAIRS (build knob): a binary node whose two children are triangles
+// becomes one leaf of two contiguous triangles (bvh.hip, k_leaf_place); leaf
+// codes are then ~(slot << 1 | count - 1). Off: ~slot, one triangle per leaf.
+#ifndef PM_BVH_PAIRS
+#define PM_BVH_PAIRS 0
+#endif
+static_assert(!(PM_BVH_PAIRS && PM_BVH_WIDTH == 8), "paired leaves are laid out for the BVH4 collapse only");
 template <bool ANY>
 __device__ __forceinline__ bool leaf_test(const DevScene& S, const Ray& r, float tmin, float tmax, int code,
                                           HitInfo& h) {
+  if (PM_BVH_PAIRS) {
+    const int v = ~code, slot = v >> 1;
+    const bool h0 =
+        leaf_hit<ANY>(S.tri[3 * slot + 0], S.tri[3 * slot + 1], S.tri[3 * slot + 2], r, tmin, tmax, slot, h);
+    if (ANY && h0) return true;
+    if (v & 1) {
+      const int s1 = slot + 1;
+      const bool h1 = leaf_hit<ANY>(S.tri[3 * s1 + 0], S.tri[3 * s1 + 1], S.tri[3 * s1 + 2], r, tmin, tmax, s1, h);
+      return h0 || h1;
+    }
+    return h0;
+  }
   const int slot = ~code;
   return leaf_hit<ANY>(S.tri[3 * slot + 0], S.tri[3 * slot + 1], S.tri[3 * slot + 2], r, tmin, tmax, slot, h);
 }
