@@ -494,6 +494,10 @@ __device__ __forceinline__ float level_cut(const float4* __restrict__ lead, int6
     if (jp >= 1) b = fmin(b, seed_bound(lead[(jp - 1) * ls], q));
     if (jp + 2 < ns) b = fmin(b, seed_bound(lead[(jp + 2) * ls], q));
   }
+  if (PM_SEED_LEADERS > 4) {
+    if (jp >= 2) b = fmin(b, seed_bound(lead[(jp - 2) * ls], q));
+    if (jp + 3 < ns) b = fmin(b, seed_bound(lead[(jp + 3) * ls], q));
+  }
   return seed_cut(b, R2);
 }
 
