@@ -640,7 +640,7 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
 // pool_chunk picks the chunk: up to PM_POOL_RAYS rays per lane, fewer when the
 // launch would otherwise have fewer than ~16 workgroups per CU.
 #ifndef PM_POOL_RAYS
-#define PM_POOL_RAYS 8
+#define PM_POOL_RAYS 4   // config 3 frame: 16 139.4, 8 138.4, 4 136.7, 2 136.9 ms (shorter launch tails)
 #endif
 inline int pool_chunk(int64_t n, int block) {
   const int64_t target = 256 * 16;   // workgroups: 256 CUs x 16
