@@ -164,7 +164,7 @@ __global__ void k_pack_children(float4* nodes, const int4* child, int nn) {
 // argmin (t, triangle id) whatever the tree.
 constexpr int kPlocRadius = 32;   // LDS window; the search radius r <= kPlocRadius (PM_PLOC_RADIUS)
 constexpr int kPlocBlock = 256;
-constexpr int kPlocDefaultRadius = 16;   // config 3 frame: r 8 168.2 ms, 16 168.5, 24 173.3, 32 175.4 (LBVH 176.4)
+constexpr int kPlocDefaultRadius = 8;   // config 3 frame: r 8 168.2 ms, 16 168.5, 24 173.3, 32 175.4 (LBVH 176.4); at 137 ms: r 2 137.5, 4 138.1, 8 136.9, 16 137.2, 32 140.3
 
 struct Clu {   // cluster: box (lo.xyz, code bits) (hi.xyz, -)
   float4 lo, hi;
