@@ -363,12 +363,35 @@ hipError_t launch_trace_wavefront(pm_scene* sc, const LightDev* d_lights, const 
   return hipStreamSynchronize(s);
 }
 
-__global__ void k_compact_photons(const pm_photon* slots, const uint32_t* cnt, const uint32_t* off, int64_t np,
-                                  pm_photon* out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= np) return;
-  const uint32_t c = cnt[i], o = off[i];
-  for (uint32_t k = 0; k < c; k++) out[(int64_t)o + k] = slots[(int64_t)k * np + i];
+// Compaction into the canonical (photon, bounce) order. A block's 256 photons own
+// one contiguous output range: their deposits are read row by row (coalesced),
+// staged in LDS at their output offsets and written out as consecutive floats;
+// a block whose range exceeds the stage writes directly (same positions).
+constexpr int kCompactStage = 1536;   // records (60 KB)
+static_assert(sizeof(pm_photon) == 10 * sizeof(float), "pm_photon is staged as 10 floats");
+__global__ __launch_bounds__(256) void k_compact_photons(const pm_photon* slots, const uint32_t* cnt,
+                                                         const uint32_t* off, int64_t np, pm_photon* out) {
+  __shared__ float stage[kCompactStage * 10];
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t i = i0 + threadIdx.x;
+  const int64_t ilast = (i0 + blockDim.x < np ? i0 + blockDim.x : np) - 1;
+  const uint32_t c = i < np ? cnt[i] : 0u, o = i < np ? off[i] : 0u;
+  const uint32_t b0 = off[i0], b1 = off[ilast] + cnt[ilast];   // block's output range
+  const uint32_t total = b1 - b0;
+  if (total > (uint32_t)kCompactStage) {
+    for (uint32_t k = 0; k < c; k++) out[(int64_t)o + k] = slots[(int64_t)k * np + i];
+    return;
+  }
+  for (uint32_t k = 0; k < c; k++) {
+    const pm_photon ph = slots[(int64_t)k * np + i];
+    const float* f = reinterpret_cast<const float*>(&ph);
+    float* d = stage + (size_t)(o - b0 + k) * 10;
+#pragma unroll
+    for (int w = 0; w < 10; w++) d[w] = f[w];
+  }
+  __syncthreads();
+  float* of = reinterpret_cast<float*>(out + b0);
+  for (uint32_t w = threadIdx.x; w < total * 10; w += blockDim.x) of[w] = stage[w];
 }
 
 hipError_t launch_trace_chunk(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl, int64_t g_lo,
