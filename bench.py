@@ -38,6 +38,25 @@ def knn_query_bytes(n_photons: int, k: int = 50) -> int:
     return 16 * math.ceil(math.log2(max(2, n_photons))) + 28 * k + 24
 
 
+def host_cores():
+    """(threads to use, os.cpu_count(), affinity-mask CPUs, cgroup CPU quota or None).
+    The CPU baseline runs on every CPU this process may use: the affinity mask,
+    capped by the cgroup v2 CPU quota when one is set (extra threads beyond a
+    quota only time-slice)."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        quota = None
+    use = aff if quota is None else max(1, min(aff, math.ceil(quota)))
+    return use, nproc, aff, quota
+
+
 def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
     """Scalar oracle (oracle/libpm_oracle.so, pthreads) on a bounded sample of the
     same workload, scaled linearly to one frame."""
@@ -56,8 +75,8 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
     c = oracle.trace(sc, lights, args.caustic, args.max_depth, True, nthreads=nthreads, g_range=(0, scn))
     t_trace = (time.time() - t) / frac
     t = time.time()
-    gm = oracle.PhotonMap(g, 1.0, c, 0.5)
-    cm = oracle.PhotonMap(c, 0.5)
+    gm = oracle.PhotonMap(g, 1.0, c, 0.5, nthreads=nthreads)
+    cm = oracle.PhotonMap(c, 0.5, nthreads=nthreads)
     t_build_s = time.time() - t
     n_s = max(2, len(g) + len(c))
     t_build = t_build_s * (n_global_full / n_s) * (math.log2(max(2, n_global_full)) / math.log2(n_s))
@@ -70,8 +89,10 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
                   rows=(r0, r0 + rows), nthreads=nthreads, caustic_k=args.caustic_k)
     t_render = (time.time() - t) * args.height / rows
     total = t_trace + t_build + t_render
+    _, nproc, aff, quota = host_cores()
     return {
         "value": P / total / 1e6, "unit": "Mphotons/s", "cores": nthreads, "kind": "port",
+        "nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
         "sample": (f"oracle (pthreads x{nthreads}) traced {sg + scn} of {P} photons (scaled x{1 / frac:.1f}), "
                    f"kd-built {n_s} photons (scaled N log N to {n_global_full}), rendered {rows} of "
                    f"{args.height} rows at {args.width} px (scaled x{args.height / rows:.1f}) with the sampled "
@@ -99,7 +120,8 @@ def main():
     ap.add_argument("--depth", type=int, default=30)
     ap.add_argument("--scene", default="sponza", choices=["sponza", "cornell"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: every CPU this process may use, see host_cores)")
     ap.add_argument("--cpu-sample-photons", type=int, default=2_000_000)
     ap.add_argument("--cpu-sample-rows", type=int, default=48)
     args = ap.parse_args()
@@ -243,7 +265,8 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(meshes, lights, args, info["n_global"], args.cpu_threads)
+        out["cpu_baseline"] = cpu_baseline(meshes, lights, args, info["n_global"],
+                                           args.cpu_threads or host_cores()[0])
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -97,6 +97,7 @@ def _load():
                                              C.c_int64, C.c_int32, _P, C.c_int64, C.POINTER(C.c_int64)]),
         "orc_map_create": (C.c_int, [_P, C.c_int64, C.c_float, _P, C.c_int64, C.c_float, C.POINTER(_P)]),
         "orc_map_destroy": (None, [_P]),
+        "orc_set_build_threads": (None, [C.c_int32]),
         "orc_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_float, C.c_int32, _P, _P, _P]),
         "orc_gather": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, _P]),
         "orc_gather_k": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P]),
@@ -217,11 +218,12 @@ def trace(scene: Scene, lights, casted, max_depth, caustics, shard_rank=0, shard
 
 
 class PhotonMap:
-    def __init__(self, a: np.ndarray, pa: float, b: np.ndarray = None, pb: float = 0.0):
+    def __init__(self, a: np.ndarray, pa: float, b: np.ndarray = None, pb: float = 0.0, nthreads: int = 1):
         a = np.ascontiguousarray(a if a is not None else np.zeros((0, 10), np.float32), np.float32)
         b = np.ascontiguousarray(b if b is not None else np.zeros((0, 10), np.float32), np.float32)
         self._keep = (a, b)
         h = _P()
+        lib.orc_set_build_threads(int(nthreads))
         _chk(lib.orc_map_create(a.ctypes.data if len(a) else None, len(a), float(pa),
                                 b.ctypes.data if len(b) else None, len(b), float(pb), C.byref(h)), "map_create")
         self.h = h

@@ -690,18 +690,48 @@ struct orc_map {
   int32_t* node_lo; int32_t* node_hi; int8_t* node_dim; float* node_split; int32_t nnodes;
 };
 
-/* ray-tracer/src/hostCode.cu:54-83 loadPhotons: map = a (power_a) ++ b (power_b) */
-static int ocmp_dim;
-static const float* ocmp_pos;
-static int ocmp(const void* a, const void* b) {
-  int32_t ia = *(const int32_t*)a, ib = *(const int32_t*)b;
-  float ca = ocmp_pos[(int64_t)ia * 3 + ocmp_dim], cb = ocmp_pos[(int64_t)ib * 3 + ocmp_dim];
-  if (ca < cb) return -1;
-  if (ca > cb) return 1;
-  return ia < ib ? -1 : (ia > ib);
+/* ray-tracer/src/hostCode.cu:54-83 loadPhotons: map = a (power_a) ++ b (power_b).
+ * Build: median split on the widest dimension in (coord, original index) order,
+ * found by quickselect (O(n) per level; the subtree MEMBERSHIP equals a full
+ * sort's, so the tree is independent of the selection method), subtrees built
+ * in parallel threads near the root (the CPU baseline uses every core). */
+static inline int kd_less(const float* pos, int dim, int32_t a, int32_t b) {
+  const float ca = pos[(int64_t)a * 3 + dim], cb = pos[(int64_t)b * 3 + dim];
+  return ca < cb || (ca == cb && a < b);
 }
-/* Node layout: implicit binary tree over the idx array, leaves <= 8 points. */
-static void kd_build(orc_map* m, int32_t node, int64_t lo, int64_t hi) {
+/* rearranges v[0..n) so that v[k] is the k-th smallest and v[<k] <= v[k] <= v[>k] */
+static void kd_select(const float* pos, int dim, int32_t* v, int64_t n, int64_t k) {
+  int64_t lo = 0, hi = n - 1;
+  while (hi > lo) {
+    /* median-of-three pivot */
+    const int64_t mid = lo + (hi - lo) / 2;
+    int32_t a = v[lo], b = v[mid], c = v[hi], pv;
+    if (kd_less(pos, dim, a, b)) pv = kd_less(pos, dim, b, c) ? b : (kd_less(pos, dim, a, c) ? c : a);
+    else pv = kd_less(pos, dim, a, c) ? a : (kd_less(pos, dim, b, c) ? c : b);
+    int64_t i = lo, j = hi;
+    while (i <= j) {
+      while (kd_less(pos, dim, v[i], pv)) i++;
+      while (kd_less(pos, dim, pv, v[j])) j--;
+      if (i <= j) {
+        const int32_t t = v[i]; v[i] = v[j]; v[j] = t;
+        i++; j--;
+      }
+    }
+    if (k <= j) hi = j;
+    else if (k >= i) lo = i;
+    else return;
+  }
+}
+typedef struct { orc_map* m; int32_t node; int64_t lo, hi; int par; } kd_task;
+static void kd_build(orc_map* m, int32_t node, int64_t lo, int64_t hi, int par);
+static void* kd_build_thread(void* arg) {
+  kd_task* t = (kd_task*)arg;
+  kd_build(t->m, t->node, t->lo, t->hi, t->par);
+  return NULL;
+}
+/* Node layout: implicit binary tree over the idx array, leaves <= 8 points.
+ * par > 1: build the left child in a new thread (par/2 threads each side). */
+static void kd_build(orc_map* m, int32_t node, int64_t lo, int64_t hi, int par) {
   m->node_lo[node] = (int32_t)lo;
   m->node_hi[node] = (int32_t)hi;
   if (hi - lo <= 8 || 2 * node + 2 >= m->nnodes) { m->node_dim[node] = -1; return; }
@@ -713,14 +743,26 @@ static void kd_build(orc_map* m, int32_t node, int64_t lo, int64_t hi) {
     }
   int dim = 0;
   for (int k = 1; k < 3; k++) if (mx[k] - mn[k] > mx[dim] - mn[dim]) dim = k;
-  ocmp_dim = dim; ocmp_pos = m->pos;
-  qsort(&m->idx[lo], (size_t)(hi - lo), sizeof(int32_t), ocmp);
-  int64_t mid = lo + (hi - lo) / 2;
+  const int64_t mid = lo + (hi - lo) / 2;
+  kd_select(m->pos, dim, &m->idx[lo], hi - lo, mid - lo);
   m->node_dim[node] = (int8_t)dim;
   m->node_split[node] = m->pos[(int64_t)m->idx[mid] * 3 + dim];
-  kd_build(m, 2 * node + 1, lo, mid);
-  kd_build(m, 2 * node + 2, mid, hi);
+  if (par > 1 && hi - lo > 65536) {
+    kd_task t = {m, 2 * node + 1, lo, mid, par / 2};
+    pthread_t th;
+    if (pthread_create(&th, NULL, kd_build_thread, &t) == 0) {
+      kd_build(m, 2 * node + 2, mid, hi, par - par / 2);
+      pthread_join(th, NULL);
+      return;
+    }
+  }
+  kd_build(m, 2 * node + 1, lo, mid, 1);
+  kd_build(m, 2 * node + 2, mid, hi, 1);
 }
+
+/* threads of the map build (orc_set_build_threads; default 1) */
+static int orc_build_threads = 1;
+void orc_set_build_threads(int32_t n) { orc_build_threads = n < 1 ? 1 : (n > 256 ? 256 : n); }
 
 int orc_map_create(const pm_photon* a, int64_t na, float power_a,
                    const pm_photon* b, int64_t nb, float power_b, orc_map** out) {
@@ -746,7 +788,7 @@ int orc_map_create(const pm_photon* a, int64_t na, float power_a,
   m->node_hi = (int32_t*)calloc((size_t)m->nnodes, sizeof(int32_t));
   m->node_dim = (int8_t*)calloc((size_t)m->nnodes, sizeof(int8_t));
   m->node_split = (float*)calloc((size_t)m->nnodes, sizeof(float));
-  kd_build(m, 0, 0, n);
+  kd_build(m, 0, 0, n, orc_build_threads);
   *out = m;
   return PM_OK;
 }

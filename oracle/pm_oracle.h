@@ -60,6 +60,8 @@ int orc_trace_photon_range(const orc_scene* s, const pm_light* lights, int32_t n
                            int64_t* count);
 
 /* --- stage 2 --- */
+/* threads used by orc_map_create's kd build (default 1) */
+void orc_set_build_threads(int32_t n);
 int orc_map_create(const pm_photon* a, int64_t na, float power_a,
                    const pm_photon* b, int64_t nb, float power_b, orc_map** out);
 void orc_map_destroy(orc_map* m);

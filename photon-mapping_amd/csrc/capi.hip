@@ -389,10 +389,9 @@ int pm_trace_photons(pm_scene* sc, const pm_light* lights, int32_t nl, const pm_
 
 // ------------------------------------------------------------------ stage 2
 int pm_kdtree_build(pm_kd_photon* d, int64_t n, pm_box* bounds, void* stream) {
-  if (n < 0 || (n > 0 && !d)) return PM_ERR_INVALID;
+  if (n < 0 || (n > 0 && !d) || n >= kMaxMapPhotons) return PM_ERR_INVALID;
   int st = require_device();
   if (st != PM_OK) return st;
-  if (n >= (1ll << 30)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
   reset_phase(PH_KDBUILD);
@@ -404,10 +403,10 @@ int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_phot
                          pm_photon_map** out, void* stream) {
   if (!out || na < 0 || nb < 0 || (na > 0 && !a) || (nb > 0 && !b)) return PM_ERR_INVALID;
   *out = nullptr;
+  const int64_t n = na + nb;
+  if (n >= kMaxMapPhotons) return PM_ERR_INVALID;
   int st = require_device();
   if (st != PM_OK) return st;
-  const int64_t n = na + nb;
-  if (n >= (1ll << 30)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
   pm_photon_map* m = new pm_photon_map;
@@ -469,10 +468,10 @@ int pm_kd_shard_plan_create(const pm_photon* a, int64_t na, float pa, const pm_p
                             int32_t world, pm_kd_shard_plan** out, void* stream) {
   if (!out || na < 0 || nb < 0 || world < 1 || (na > 0 && !a) || (nb > 0 && !b)) return PM_ERR_INVALID;
   *out = nullptr;
+  const int64_t n = na + nb;
+  if (n >= kMaxMapPhotons) return PM_ERR_INVALID;
   int st = require_device();
   if (st != PM_OK) return st;
-  const int64_t n = na + nb;
-  if (n >= (1ll << 30)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
   pm_kd_shard_plan* p = new pm_kd_shard_plan;

@@ -271,6 +271,7 @@ bool load_glb(const std::string& path, RawScene& sc, std::string& err) {
     if (!accessors || ai < 0 || ai >= (int)accessors->arr.size()) return false;
     const JVal& a = accessors->arr[ai];
     count = (int)a.n("count", 0);
+    if (count < 0) return false;   // malformed: a negative count would skip the bounds check
     ctype = (int)a.n("componentType", 0);
     const JVal* ty = a.get("type");
     std::string t = ty ? ty->str : "";
@@ -474,16 +475,28 @@ extern "C" int pm_scene_data_load(const char* cpath, pm_scene_data** out) {
   }
   std::unique_ptr<pm_scene_data> S(new pm_scene_data);
   // extract_objects: BFS, transform = node * parent
+  // glTF node graphs are trees: a node reached twice (a cycle, or two parents)
+  // is malformed and rejected instead of looping forever
   std::deque<std::pair<int, Mat4>> q;
+  std::vector<char> seen(sc.nodes.size(), 0);
   q.emplace_back(sc.root, Mat4::identity());
   while (!q.empty()) {
     auto [ni, parent] = q.front();
     q.pop_front();
     if (ni < 0 || ni >= (int)sc.nodes.size()) continue;
+    if (seen[ni]) {
+      std::fprintf(stderr, "pm: scene import failed: node %d is reached twice (cyclic node hierarchy)\n", ni);
+      return PM_ERR_IO;
+    }
+    seen[ni] = 1;
     const RawNode& node = sc.nodes[ni];
     const Mat4 T = mul(node.M, parent);
     for (int c : node.children) q.emplace_back(c, T);
     for (int mi : node.meshes) {
+      if (mi < 0 || mi >= (int)sc.meshes.size()) {
+        std::fprintf(stderr, "pm: scene import failed: node %d names mesh %d of %zu\n", ni, mi, sc.meshes.size());
+        return PM_ERR_IO;
+      }
       const RawMesh& rm = sc.meshes[mi];
       std::vector<pm_float3> verts;
       std::vector<pm_int3> idx;

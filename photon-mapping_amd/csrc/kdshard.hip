@@ -51,7 +51,7 @@ __device__ __forceinline__ int top_path(const float4 e, const float4* __restrict
   int t = 0;
   for (int k = 0; k < l; k++) {
     const float4 nd = top[t];
-    const int w = __float_as_int(nd.w), dim = w & 3, nid = w >> 2;
+    const int w = __float_as_int(nd.w), dim = w & 3, nid = (int)((uint32_t)w >> 2);
     if (id == nid) return -1;
     const float c = shard_coord(e, dim), nc = shard_coord(nd, dim);
     const bool left = c < nc || (c == nc && id < nid);
@@ -291,7 +291,7 @@ __global__ void k_shard_tags(const float4* __restrict__ nodes, int64_t s, const 
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= s) return;
   const int w = __float_as_int(nodes[u].w);
-  tags[u] = (gid[w >> 2] << 2) | (w & 3);
+  tags[u] = (gid[(uint32_t)w >> 2] << 2) | (w & 3);
 }
 
 // subtree rooted at global node t: local node u (depth d, k-th at that depth)
@@ -303,7 +303,7 @@ __global__ void k_shard_place(const float4* __restrict__ elems, const int32_t* _
   const int d = 63 - __clzll((unsigned long long)(u + 1));
   const int64_t k = u + 1 - ((int64_t)1 << d);
   const int w = tags[u];
-  const float4 e = elems[w >> 2];
+  const float4 e = elems[(uint32_t)w >> 2];
   nodes[(t + 1) * ((int64_t)1 << d) - 1 + k] = make_float4(e.x, e.y, e.z, __int_as_float(w));
 }
 
@@ -316,7 +316,7 @@ int shard_levels(int world) {
   return std::min(L + 1, kShardMaxLevels);
 }
 
-bool shard_ok(int64_t n, int L) { return L >= 1 && L <= kShardMaxLevels && n >= (2ll << L) && n < (1ll << 30); }
+bool shard_ok(int64_t n, int L) { return L >= 1 && L <= kShardMaxLevels && n >= (2ll << L) && n < kMaxMapPhotons; }
 
 // Top L levels: top[0 .. 2^L - 1) and the 2^L subtree sizes (host).
 hipError_t kd_shard_top(const float4* elems, int64_t n, int L, float4* top, std::vector<int64_t>& sizes,

@@ -526,7 +526,7 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 
 hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  if (n >= (1ll << 30)) return hipErrorInvalidValue;
+  if (n >= kMaxMapPhotons) return hipErrorInvalidValue;
   int H = 0;
   while ((1ll << H) <= n) H++;          // levels = floor(log2 n) + 1
   const int64_t cap = 1ll << (H + 1);
@@ -614,7 +614,7 @@ __global__ void k_kd_reorder(const pm_kd_photon* src, const float4* nodes, int64
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const int w = __float_as_int(nodes[t].w);
-  pm_kd_photon p = src[w >> 2];
+  pm_kd_photon p = src[(uint32_t)w >> 2];
   p.split_dim = (uint8_t)(w & 3);
   dst[t] = p;
 }
@@ -624,7 +624,7 @@ __global__ void k_map_export(const float4* nodes, const float4* payload, int64_t
   if (t >= n) return;
   const float4 nd = nodes[t];
   const int w = __float_as_int(nd.w);
-  const float4 pl = payload[w >> 2];
+  const float4 pl = payload[(uint32_t)w >> 2];
   pm_kd_photon p;
   p.pos = {nd.x, nd.y, nd.z};
   p.dir = {0.f, 0.f, 0.f};

@@ -116,7 +116,7 @@ __device__ __forceinline__ void knn_walk(const float4* __restrict__ nodes, int n
       if (test) {
         const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
         const float d2 = dx * dx + dy * dy + dz * dz;
-        key = key_make(d2, (uint32_t)(w >> 2));
+        key = key_make(d2, (uint32_t)w >> 2);
         cand = d2 < r2 && key < list[K - 1] && key > lo;
       }
       int next;
@@ -257,7 +257,7 @@ __device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, int 
   const bool down = w.prev < child;
   const bool test = (down && close_c >= n) || w.prev == close_c;
   const float d2 = dx * dx + dy * dy + dz * dz;
-  const double key = key_make(d2, (uint32_t)(wd >> 2));
+  const double key = key_make(d2, (uint32_t)wd >> 2);
   const bool cand = w.walking && test && key < list[K - 1];
   int next, nprev;
   if (JUMP) {

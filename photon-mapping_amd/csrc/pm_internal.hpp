@@ -40,6 +40,11 @@ struct pm_photon_map {
 
 namespace pmd {
 
+// Largest photon map / kd-tree: node tags are int32 (original index << 2 | split
+// dimension), so every original index must stay below 2^29 for the tag to stay
+// non-negative (ids >= 2^29 would sign-extend when decoded).
+constexpr int64_t kMaxMapPhotons = int64_t(1) << 29;
+
 // Light for the photon tracer: pos.xyz, rgb.xyz, rgb.w = type (0 point,
 // 1 square), nrm = (normal.xyz, side length).
 struct LightDev {

@@ -479,8 +479,10 @@ class PhotonMap:
 
 class KdShardPlan:
     """The global map's tree split across `world` ranks (pm_kd_shard_plan_*,
-    SURVEY §8e): top levels selected here, subtree j built by rank j % world,
-    subtrees all-gathered by the caller, then `map(all_subtrees)`."""
+    SURVEY §8e): top levels selected here; the subtrees are dealt to ranks by
+    `pm_amd.dist.shard_owners(plan.sizes, world)` (size-balanced, deterministic),
+    each rank builds its own (`build`), the caller all-gathers them and
+    `map(all_subtrees)` places them (subtree order)."""
 
     def __init__(self, a, power_a: float, b=None, power_b: float = 0.0, world: int = 1, stream=None):
         h = _P()
@@ -635,8 +637,9 @@ class RenderJob:
 
 
 def render_begin(scene: Scene, camera: Camera, width: int, height: int, spp: int, depth: int, sky, lights,
-                 tile_rank: int = 0, tile_count: int = 1, stream=None) -> RenderJob:
-    return RenderJob(scene, camera, width, height, spp, depth, sky, lights, tile_rank, tile_count, stream)
+                 tile_rank: int = 0, tile_count: int = 1, stream=None, caustic_k: int = 0) -> RenderJob:
+    return RenderJob(scene, camera, width, height, spp, depth, sky, lights, tile_rank, tile_count, stream,
+                     caustic_k=caustic_k)
 
 
 def view_photons(scene: Scene, photons, look_from, look_at, look_up, fovy: float, width: int, height: int,

@@ -52,8 +52,27 @@ def shard_range(total: int, rank: int, world: int):
     return total * rank // world, total * (rank + 1) // world
 
 
-def allgather_rows(t, world: int, dist):
-    """Variable-length all-gather of an (n_r, C) tensor, concatenated in rank order."""
+class _Gathered:
+    """An all-gather in flight (allgather_rows_start); wait() returns the rows
+    concatenated in rank order."""
+
+    def __init__(self, work, out, ns, m, world, parts=None):
+        self.work, self.out, self.ns, self.m, self.world, self.parts = work, out, ns, m, world, parts
+
+    def wait(self):
+        import torch
+        if self.work is not None:
+            self.work.wait()
+        if self.parts is None:
+            self.parts = [self.out[r * self.m: r * self.m + self.ns[r]] for r in range(self.world)]
+        return torch.cat(self.parts)
+
+
+def allgather_rows_start(t, world: int, dist):
+    """Variable-length all-gather of an (n_r, C) tensor: the counts are exchanged
+    first (the host sizes the padded buffer), then ONE padded all-gather is
+    started asynchronously on device tensors (RCCL runs it on its own stream, so
+    the caller can overlap work on the current stream until wait())."""
     import torch
     n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
     ns = [torch.zeros_like(n) for _ in range(world)]
@@ -64,13 +83,39 @@ def allgather_rows(t, world: int, dist):
     pad[: t.shape[0]] = t
     if t.device.type == "cuda":
         out = torch.empty((world * m, t.shape[1]), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, pad)
-        parts = [out[r * m: r * m + ns[r]] for r in range(world)]
-    else:
-        bufs = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(bufs, pad)
-        parts = [bufs[r][: ns[r]] for r in range(world)]
-    return torch.cat(parts)
+        work = dist.all_gather_into_tensor(out, pad, async_op=True)
+        return _Gathered(work, out, ns, m, world)
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad)
+    return _Gathered(None, None, ns, m, world, parts=[bufs[r][: ns[r]] for r in range(world)])
+
+
+def allgather_rows(t, world: int, dist):
+    """Variable-length all-gather of an (n_r, C) tensor, concatenated in rank order."""
+    return allgather_rows_start(t, world, dist).wait()
+
+
+class _PhaseClock:
+    """Elapsed time of a phase: HIP events on the current stream for device work
+    (collectives included: a finished RCCL call makes the current stream wait
+    for it), wall clock for host tensors."""
+
+    def __init__(self, cuda: bool):
+        import torch
+        self.cuda = cuda
+        if cuda:
+            self.a = torch.cuda.Event(enable_timing=True)
+            self.b = torch.cuda.Event(enable_timing=True)
+            self.a.record()
+        else:
+            self.t0 = time.perf_counter()
+
+    def stop_us(self) -> float:
+        if not self.cuda:
+            return (time.perf_counter() - self.t0) * 1e6
+        self.b.record()
+        self.b.synchronize()
+        return self.a.elapsed_time(self.b) * 1e3
 
 
 class HostStagedDist:
@@ -89,15 +134,17 @@ class HostStagedDist:
         for o, h in zip(outs, hs):
             o.copy_(h)
 
-    def all_gather_into_tensor(self, out, t):
+    def all_gather_into_tensor(self, out, t, async_op=False):
         h = self.t.empty_like(out, device="cpu")
         self.d.all_gather_into_tensor(h, t.cpu())
         out.copy_(h)
+        return None   # completed (host-staged): nothing to wait for
 
     def reduce(self, t, dst, op):
         h = t.cpu()
         self.d.reduce(h, dst=dst, op=op)
-        t.copy_(h)
+        if self.d.get_rank() == dst:   # only the root's buffer receives the result
+            t.copy_(h)
 
     def all_reduce(self, t, op):
         h = t.cpu()
@@ -177,11 +224,10 @@ def sharded_map(pm, g, c, rank: int, world: int, dist):
         m = plan.map()
         return m, us + pm.phase_us("kdbuild")
     local, bus = shard_local(plan, rank, world)
-    t0 = time.time()
+    clock = _PhaseClock(local.device.type == "cuda")
     everyone = torch.empty((world * local.shape[0],), dtype=torch.int32, device=local.device)
     dist.all_gather_into_tensor(everyone, local)
-    torch.cuda.synchronize()
-    xus = (time.time() - t0) * 1e6
+    xus = clock.stop_us()
     m = shard_assemble(plan, everyone, world)
     us += bus + xus + pm.phase_us("kdbuild")
     plan.close()
@@ -217,16 +263,21 @@ class GpuBackend:
     def quantize(self, t):
         return self.pm.quantize_photons(t)
 
-    def maps(self, g, c, rank: int = 0, world: int = 1, dist=None):
+    def caustic_map(self, c):
+        pm = self.pm
+        cm = pm.PhotonMap(c, pm.CAUSTICS_PHOTON_POWER)
+        self.phase["kdbuild"] = self.phase.get("kdbuild", 0.0) + pm.phase_us("kdbuild")
+        return cm
+
+    def global_map(self, g, c, rank: int = 0, world: int = 1, dist=None):
         pm = self.pm
         if world > 1 and self.cfg.shard_build:
             gm, kd = sharded_map(pm, g, c, rank, world, dist)
         else:
             gm = pm.PhotonMap(g, pm.PHOTON_POWER, c, pm.CAUSTICS_PHOTON_POWER)
             kd = pm.phase_us("kdbuild")
-        cm = pm.PhotonMap(c, pm.CAUSTICS_PHOTON_POWER)
-        self.phase["kdbuild"] = kd + pm.phase_us("kdbuild")
-        return gm, cm
+        self.phase["kdbuild"] = self.phase.get("kdbuild", 0.0) + kd
+        return gm
 
     def render(self, gm, cm, tile_rank: int, tile_count: int, rgba):
         pm = self.pm
@@ -239,23 +290,30 @@ class GpuBackend:
 
 
 def frame(backend, rank: int, world: int, dist=None, rgba=None):
-    """One frame through `backend`; returns (rgba on rank 0 (merged), info)."""
-    import torch
+    """One frame through `backend`; returns (rgba on rank 0 (merged), info).
+    N > 1: the caustic photons are exchanged first (small), then the global
+    photons' all-gather runs on RCCL's stream while the caustic map is built;
+    phases_us["exchange"] is that window (HIP events), caustic build included."""
     backend.phase = {}
     g = backend.trace(False, rank, world)
     c = backend.trace(True, rank, world)
     if backend.cfg.quantize:   # elementwise: the same before or after the exchange
         g, c = backend.quantize(g), backend.quantize(c)
-    te = time.time()
     if world > 1:
         # only position and colour reach the maps (kd nodes + gather payload):
         # 24 of the 40 bytes of a photon cross xGMI
-        g = unpack_rows(allgather_rows(pack_rows(g), world, dist))
+        clock = _PhaseClock(g.device.type == "cuda")
         c = unpack_rows(allgather_rows(pack_rows(c), world, dist))
-        if g.device.type == "cuda":
-            torch.cuda.synchronize()
-    backend.phase["exchange"] = (time.time() - te) * 1e6
-    gm, cm = backend.maps(g, c, rank, world, dist)
+        pending = allgather_rows_start(pack_rows(g), world, dist)
+        cm = backend.caustic_map(c)   # overlaps the global photons' transfer
+        g = unpack_rows(pending.wait())
+        backend.phase["exchange"] = clock.stop_us()
+    else:
+        backend.phase["exchange"] = 0.0
+        cm = backend.caustic_map(c)
+    gm = backend.global_map(g, c, rank, world, dist)
+    if world > 1 and rgba is not None:
+        rgba.zero_()   # tiles are disjoint: the SUM-reduce needs zeros outside this rank's tiles
     rgba = backend.render(gm, cm, rank, world, rgba)
     if world > 1:
         dist.reduce(rgba, dst=0, op=dist.ReduceOp.SUM)

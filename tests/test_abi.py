@@ -87,3 +87,21 @@ def test_host_helpers_without_gpu():
     assert pm_amd.trace_capacity(lights, 10000, 10, False) == 10000 * 9
     assert pm_amd.trace_capacity(lights, 10000, 10, True) == 10000
     assert pm_amd.trace_capacity(lights, 10001, 10, False, 1, 3) == (10000 * 2 // 3 - 10000 // 3) * 9
+
+
+def test_map_size_limit_rejected_before_any_work():
+    """kd node tags are int32 (original index << 2 | split dim): maps of 2^29
+    photons or more are rejected with PM_ERR_INVALID, checked
+    before the device is touched, so the guard is testable on any host."""
+    import pm_amd
+    lib = pm_amd.lib
+    fake = C.c_void_p(64)   # never dereferenced: the size check comes first
+    out = C.c_void_p()
+    for na, nb in ((1 << 29, 0), ((1 << 29) - 7, 7), (1 << 30, 0)):
+        assert lib.pm_photon_map_create(fake, na, C.c_float(1.0), fake, nb, C.c_float(0.5), C.byref(out),
+                                        None) == pm_amd.PM_ERR_INVALID
+        assert lib.pm_kd_shard_plan_create(fake, na, C.c_float(1.0), fake, nb, C.c_float(0.5), 8, C.byref(out),
+                                           None) == pm_amd.PM_ERR_INVALID
+    assert lib.pm_kdtree_build(fake, 1 << 29, None, None) == pm_amd.PM_ERR_INVALID
+    if pm_amd.device_count() == 0:   # just under the limit passes the guard and stops at the device probe
+        assert lib.pm_kdtree_build(fake, (1 << 29) - 1, None, None) == pm_amd.PM_ERR_NO_DEVICE

@@ -30,13 +30,16 @@ class OracleBackend:
                          shard_count=world, nthreads=2)
         return torch.from_numpy(a)
 
-    def maps(self, g, c, rank=0, world=1, dist=None):
-        gm = self.o.PhotonMap(g.numpy(), 1.0, c.numpy(), 0.5)
-        cm = self.o.PhotonMap(c.numpy(), 0.5)
+    def caustic_map(self, c):
+        return self.o.PhotonMap(c.numpy(), 0.5)
+
+    def global_map(self, g, c, rank=0, world=1, dist=None):
         self.last = (g.numpy().copy(), c.numpy().copy())
-        return gm, cm
+        return self.o.PhotonMap(g.numpy(), 1.0, c.numpy(), 0.5)
 
     def render(self, gm, cm, tile_rank, tile_count, rgba):
+        if rgba is not None:
+            assert int(rgba.abs().sum()) == 0, "frame() hands a zeroed buffer to every rank's render"
         c = self.cfg
         img, _, _ = self.o.render(self.scene, self.cam, c.width, c.height, c.spp, c.depth, c.sky, self.lights, gm,
                                   cm, tile_rank=tile_rank, tile_count=tile_count, nthreads=2)
@@ -56,8 +59,12 @@ def _worker(rank, world, port, q):
         import pm_amd
         from pm_amd import dist as pmdist
         meshes, lights = pm_amd.load_scene_file(conftest.CORNELL)
-        be = OracleBackend(meshes, lights, _cfg())
-        rgba, info = pmdist.frame(be, rank, world, dist)
+        cfg = _cfg()
+        be = OracleBackend(meshes, lights, cfg)
+        # a stale, non-zero frame buffer (as after a previous frame): frame() must
+        # zero it before the tile render, or the SUM-reduce would add stale pixels
+        stale = torch.full((cfg.height, cfg.width), 7, dtype=torch.int32)
+        rgba, info = pmdist.frame(be, rank, world, dist, stale)
         g, c = be.last
         q.put((rank, rgba.numpy().copy() if rank == 0 else None, g, c, info["n_global"]))
     finally:
