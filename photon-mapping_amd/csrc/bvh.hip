@@ -258,8 +258,7 @@ static hipError_t build_ploc(const float4* tri, int n, float pad, float4* bin, h
   k_ploc_leaves<<<grid_for(n, 256), 256, 0, s>>>(tri, n, pad, ca.p);
   PM_HIP_TRY(hipGetLastError());
   Clu *cur = ca.p, *nxt = cb.p;
-  const char* renv = std::getenv("PM_PLOC_RADIUS");
-  const int r = renv ? std::min(kPlocRadius, std::max(1, std::atoi(renv))) : kPlocDefaultRadius;
+  const int r = kPlocDefaultRadius;
   int m = n, top = n - 1;   // internal node ids top-1 .. 0
   while (m > 1) {
     k_ploc_nn<<<grid_for(m, kPlocBlock), kPlocBlock, 0, s>>>(cur, m, r, nn.p);
@@ -660,8 +659,9 @@ hipError_t build_lbvh(pm_scene* sc, const std::vector<float4>& th, hipStream_t s
   PM_HIP_TRY(radix_sort_pairs(codes.p, order.p, n, 30, s));
   k_gather_tris<<<grid_for(n, 256), 256, 0, s>>>(tri_orig.p, order.p, n, sc->tri.p);
   PM_HIP_TRY(hipGetLastError());
-  const char* benv = std::getenv("PM_BVH");
-  if (!(benv && std::strcmp(benv, "lbvh") == 0)) {
+  // production: PLOC clustering; the check variant builds the Karras LBVH below
+  // (a different tree: closest hits are argmin (t, id), so results must not move)
+  if (!PM_CHECK_VARIANT) {
     PM_HIP_TRY(build_ploc(sc->tri.p, n, pad, bin.p, s));
     return collapse_bvh(bin.p, nn, sc, s);
   }

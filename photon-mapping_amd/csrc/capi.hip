@@ -35,8 +35,7 @@ hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_ph
 hipError_t kd_build_records(pm_kd_photon* d, int64_t n, pm_box* bounds, hipStream_t s);
 hipError_t launch_map_export(const pm_photon_map* m, pm_kd_photon* out, hipStream_t s);
 hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int k, float radius, int32_t* ids,
-                      float* d2, float* maxd2, hipStream_t s, const float* cut1 = nullptr,
-                      const float* cut2 = nullptr);
+                      float* d2, float* maxd2, hipStream_t s);
 hipError_t launch_gather_api(const pm_photon_map* m, const pm_float3* pts, const float* brdf, int64_t nq,
                              pm_float3* out, hipStream_t s, int k);
 hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int nl, pm_render_job* J,

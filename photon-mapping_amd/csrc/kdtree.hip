@@ -14,7 +14,6 @@
 // k_kd_count -> k_kd_chunkscan / k_kd_chunkcarry -> k_kd_part). Subtree ranges are identical in the three lists, so a single tag
 // array tracks subtree membership. Ties are broken by the original index.
 #include <algorithm>
-#include <cstdlib>
 
 #include "pm_internal.hpp"
 
@@ -561,10 +560,9 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
   PM_HIP_TRY(hipMemsetAsync(tag.p, 0, sizeof(int32_t) * n, s));
   float4* cur[3] = {la[0].p, la[1].p, la[2].p};
   float4* nxt[3] = {lb[0].p, lb[1].p, lb[2].p};
-  // segments at L0 hold <= 1023 elements; PM_KD_LOCAL=0 keeps every level
-  // global (A/B and the identical-tree test)
-  const char* lenv = std::getenv("PM_KD_LOCAL");
-  const int L0 = (lenv && std::atoi(lenv) == 0) ? H : std::max(0, H - 10);
+  // segments at L0 hold <= 1023 elements; the check variant keeps every level
+  // global (the identical-tree test compares the two libraries)
+  const int L0 = PM_CHECK_VARIANT ? H : std::max(0, H - 10);
   for (int L = 0; L < H; L++) {
     if (L == L0) {
       k_kd_local<<<(int)(1ll << L0), kLocal, 0, s>>>(cur[0], cur[1], cur[2], L0, T, nodes);

@@ -642,11 +642,21 @@ __device__ __forceinline__ HitInfo traverse(const DevScene& S, const Ray& r, flo
 #ifndef PM_POOL_RAYS
 #define PM_POOL_RAYS 4   // config 3 frame: 16 139.4, 8 138.4, 4 136.7, 2 136.9 ms (shorter launch tails)
 #endif
-inline int pool_chunk(int64_t n, int block) {
+__host__ __device__ inline int pool_chunk(int64_t n, int block) {
   const int64_t target = 256 * 16;   // workgroups: 256 CUs x 16
   int64_t per = (n + target * block - 1) / (target * block);
   per = per < 1 ? 1 : (per > PM_POOL_RAYS ? PM_POOL_RAYS : per);
   return (int)(per * block);
+}
+// Workgroups that cover ANY live count n <= np when each launch picks
+// pool_chunk(n) on the device (counts that stay on the device): n / chunk(n)
+// is at most 4096 while chunk(n) < PM_POOL_RAYS * block, and largest at n = np
+// beyond that; never more than one workgroup per `block` rays.
+inline int64_t pool_grid(int64_t np, int block) {
+  const int64_t at_np = (np + pool_chunk(np, block) - 1) / pool_chunk(np, block);
+  const int64_t per_ray = (np + block - 1) / block;
+  const int64_t g = at_np > 4097 ? at_np : 4097;
+  return g < per_ray ? g : per_ray;
 }
 #ifndef PM_POOL_REFILL
 #define PM_POOL_REFILL 16

@@ -38,6 +38,17 @@ struct pm_photon_map {
   int64_t n = 0;
 };
 
+// PM_CHECK_VARIANT (build-time, tests only: lib_check/libpm_hip.so): every
+// alternate path that must give bit-identical results in one library -- the
+// plain kNN walk instead of the leader-seeded one, all-global kd levels instead
+// of the LDS finish, the Karras LBVH instead of PLOC, a one-slot first guess
+// for the render's continuation vertices (always rerun) -- plus a 4-entry LDS
+// traversal stack (PM_STACK_DEPTH=4: nearly every ray spills to scratch).
+// tests/test_gpu_check_variant.py compares it with the production library.
+#ifndef PM_CHECK_VARIANT
+#define PM_CHECK_VARIANT 0
+#endif
+
 namespace pmd {
 
 // Largest photon map / kd-tree: node tags are int32 (original index << 2 | split

@@ -620,7 +620,9 @@ hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light*
   // need); if it was short, k_paths reruns with a larger area
   static thread_local int64_t last_need = 0;
   int64_t cap = std::max<int64_t>(std::max<int64_t>(nbase, last_need + last_need / 8), 4096);
-  if (const char* ce = std::getenv("PM_RENDER_CAP")) cap = std::max<int64_t>(1, std::atoll(ce));   // tests: force a rerun
+#if PM_CHECK_VARIANT
+  cap = 1;   // check variant: the first guess is always short, so every render exercises the rerun
+#endif
   uint32_t used = 0;
   for (int attempt = 0;; attempt++) {
     const int64_t NV = nbase + cap, NG = NV * kNumDiffuseSamples, NS = NV * nl;

@@ -181,24 +181,6 @@ def test_kdtree_build_left_balanced(n):
     _check_left_balanced(out[:, :3], dims.astype(np.int64))
 
 
-@pytest.mark.parametrize("n", [5, 1023, 1024, 70000])
-def test_kdtree_local_finish_identical(n, monkeypatch):
-    """The LDS finishing kernel (bottom <= 10 levels) builds the same tree as
-    the all-global level loop."""
-    import pm_amd
-    rng = np.random.default_rng(100 + n)
-    rec = np.zeros((n, 11), np.float32)
-    rec[:, 0:3] = rng.uniform(-20, 20, size=(n, 3))
-    rec[: n // 7, 2] = 1.5          # ties on one axis
-    out = []
-    for local in ("1", "0"):
-        monkeypatch.setenv("PM_KD_LOCAL", local)
-        t = torch.from_numpy(rec.copy()).cuda()
-        pm_amd.build_tree(t)
-        out.append(t.cpu().numpy().view(np.uint32))
-    assert np.array_equal(out[0], out[1])
-
-
 def _brute_knn(pts, q, k, r):
     # same float32 evaluation order as the spec: (dx*dx + dy*dy) + dz*dz
     diff = (q[:, None, :] - pts[None, :, :]).astype(np.float32)
@@ -434,86 +416,29 @@ def test_frame_driver_matches_direct_pipeline(cornell):
         assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("mode", ["0", "4", "5", "9", "10", "11", "12", "13", "14"])
-def test_gather_modes_bitwise(cornell, monkeypatch, mode):
-    """Every PM_GATHER_MODE walk returns the default gather's bits (pm_gather
-    and a render), incl. on an empty map."""
-    import pm_amd
-    meshes, lights = cornell
-    gs = pm_amd.Scene(meshes)
-    g = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, False)
-    c = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, True)
-    gm, cm = pm_amd.load_photons(g, c)
-    rng = np.random.default_rng(7)
-    gn = g.cpu().numpy()
-    q = gn[rng.integers(0, len(gn), 4000), 0:3] + rng.normal(scale=2.0, size=(4000, 3)).astype(np.float32)
-    q = torch.from_numpy(q.astype(np.float32)).cuda()
-    brdf = torch.from_numpy(rng.uniform(0, 0.4, size=4000).astype(np.float32)).cuda()
-    empty = torch.zeros((0, 10), dtype=torch.float32, device="cuda")
-    em, _ = pm_amd.load_photons(empty, empty)
-    W, H = 40, 30
-    cam = pm_amd.setup_camera((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
-    ref = [pm_amd.gather_photons(m, q, brdf).cpu().numpy() for m in (gm, cm, em)]
-    rref = pm_amd.render(gs, cam, W, H, 1, 30, (1, 1, 1), lights, gm, cm)[1].cpu().numpy()
-    monkeypatch.setenv("PM_GATHER_MODE", mode)
-    for m, r in zip((gm, cm, em), ref):
-        assert np.array_equal(_bits(pm_amd.gather_photons(m, q, brdf).cpu().numpy()), _bits(r))
-    got = pm_amd.render(gs, cam, W, H, 1, 30, (1, 1, 1), lights, gm, cm)[1].cpu().numpy()
-    assert np.array_equal(_bits(got), _bits(rref))
-
-
-def test_render_continuation_rerun(sphere, monkeypatch):
-    """Continuation vertex slots: a 1-slot first guess overflows and the host
-    reruns k_paths with the exact count; the image and stats are unchanged."""
-    import pm_amd
-    meshes, lights = sphere
-    gs = pm_amd.Scene(meshes)
-    g = pm_amd.run_point_light_ray_gen(gs, lights, 20000, 10, False)
-    c = pm_amd.run_point_light_ray_gen(gs, lights, 20000, 10, True)
-    gmap, cmap = pm_amd.load_photons(g, c)
-    W, H = 48, 40
-    cam = pm_amd.setup_camera((80, 30, 0), (10, 20, 0), (0, 1, 0), 0.87, W, H)
-    a, ra = pm_amd.render(gs, cam, W, H, 2, 30, (1, 1, 1), lights, gmap, cmap)
-    sa = bytes(pm_amd.render_stats())
-    monkeypatch.setenv("PM_RENDER_CAP", "1")
-    b, rb = pm_amd.render(gs, cam, W, H, 2, 30, (1, 1, 1), lights, gmap, cmap)
-    assert bytes(pm_amd.render_stats()) == sa
-    assert pm_amd.render_stats().path_vertices > W * H * 2   # continuation vertices existed
-    assert torch.equal(a, b)
-    assert np.array_equal(_bits(ra.cpu().numpy()), _bits(rb.cpu().numpy()))
-
-
-@pytest.mark.parametrize("levels", [None, "256,16", "64,8,2", "xcd"])
 @pytest.mark.parametrize("jitter", [0.0, 1e-3, 0.5])
-def test_seeded_gather_tight_neighbours(cornell, monkeypatch, jitter, levels):
-    """Mode 12 (leader-seeded cut-offs) on queries in spatial order, where the
-    leader bounds are tight: queries at photon positions (d^2 = 0 ties),
-    duplicated queries and small jitters; one seed level (default) and leader
-    levels seeded by coarser leaders (PM_SEED_LEVELS),. Bitwise equal to the plain walk."""
+def test_seeded_gather_tight_neighbours(cornell, jitter):
+    """The production gather (leader-seeded cut-offs) on queries in spatial
+    order, where the leader bounds are tight: queries at photon positions
+    (d^2 = 0 ties), exact duplicates and small jitters; bitwise equal to the
+    oracle's exact kNN radiance estimate."""
+    import oracle
     import pm_amd
     meshes, lights = cornell
-    gs = pm_amd.Scene(meshes)
-    g = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, False)
-    c = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, True)
-    gm, cm = pm_amd.load_photons(g, c)
+    os_ = oracle.Scene(meshes)
+    g = oracle.trace(os_, lights, 30000, 10, False)
+    c = oracle.trace(os_, lights, 30000, 10, True)
     rng = np.random.default_rng(11)
-    gn = g.cpu().numpy()
-    q = gn[rng.integers(0, len(gn), 6000), 0:3].astype(np.float32)
+    q = g[rng.integers(0, len(g), 6000), 0:3].astype(np.float32)
     q = np.concatenate([q, q[:500]])   # exact duplicates
     q = q + (rng.normal(scale=jitter, size=q.shape).astype(np.float32) if jitter else 0)
-    q = q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))].astype(np.float32)
-    qt = torch.from_numpy(np.ascontiguousarray(q)).cuda()
-    brdf = torch.from_numpy(rng.uniform(0, 0.4, size=len(q)).astype(np.float32)).cuda()
-    monkeypatch.setenv("PM_GATHER_MODE", "11")
-    ref = [pm_amd.gather_photons(m, qt, brdf).cpu().numpy() for m in (gm, cm)]
-    if levels == "xcd":   # XCD-contiguous block ranges (PM_GATHER_XCD)
-        monkeypatch.setenv("PM_GATHER_XCD", "1")
-    elif levels:
-        monkeypatch.setenv("PM_SEED_LEVELS", levels)
-    for mode in ("12", "13", "14"):
-        monkeypatch.setenv("PM_GATHER_MODE", mode)
-        for m, r in zip((gm, cm), ref):
-            assert np.array_equal(_bits(pm_amd.gather_photons(m, qt, brdf).cpu().numpy()), _bits(r)), mode
+    q = np.ascontiguousarray(q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))].astype(np.float32))
+    brdf = rng.uniform(0, 0.4, size=len(q)).astype(np.float32)
+    for a, pa, b, pb in ((g, 1.0, c, 0.5), (c, 0.5, None, 0.0)):
+        gm = pm_amd.PhotonMap(torch.from_numpy(a).cuda(), pa, None if b is None else torch.from_numpy(b).cuda(), pb)
+        om = oracle.PhotonMap(a, pa, b, pb)
+        got = pm_amd.gather_photons(gm, torch.from_numpy(q).cuda(), torch.from_numpy(brdf).cuda()).cpu().numpy()
+        assert np.array_equal(_bits(got), _bits(om.gather(q, brdf)))
 
 
 def _synthetic_photons(n, seed, grid=None):
@@ -576,22 +501,8 @@ def test_sharded_kd_build_small_map():
     assert torch.equal(plan.map().export().view(torch.int32), ref.export().view(torch.int32))
 
 
-def test_trace_sort_knob_bitwise(cornell, monkeypatch):
-    """PM_TRACE_SORT=1 (Morton-sorted bounce rays, off by default) traces the
-    same photons bit for bit: deposit slots do not depend on processing order."""
-    import pm_amd
-    meshes, lights = cornell
-    gs = pm_amd.Scene(meshes)
-    ref = [pm_amd.run_point_light_ray_gen(gs, lights, 50000, 10, m) for m in (False, True)]
-    monkeypatch.setenv("PM_TRACE_SORT", "1")
-    got = [pm_amd.run_point_light_ray_gen(gs, lights, 50000, 10, m) for m in (False, True)]
-    for a, b in zip(ref, got):
-        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
-
-
-@pytest.mark.parametrize("seed", ["1", "0"])
 @pytest.mark.parametrize("k", [1, 8, 50, 64, 128, 129, 200, 256])
-def test_gather_k_vs_oracle(cornell, k, seed, monkeypatch):
+def test_gather_k_vs_oracle(cornell, k):
     """pm_gather_k (config 5: k = 200 caustic gather): the radiance estimate over
     the k nearest equals the oracle's bit for bit, incl. lists that do not fill."""
     import oracle
@@ -604,8 +515,7 @@ def test_gather_k_vs_oracle(cornell, k, seed, monkeypatch):
     q = np.concatenate([g[rng.integers(0, len(g), 1500), 0:3] + rng.normal(scale=0.5, size=(1500, 3)),
                         rng.uniform(-300, 300, size=(100, 3))]).astype(np.float32)   # + far queries
     brdf = rng.uniform(0, 0.4, size=len(q)).astype(np.float32)
-    q = q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))]   # spatial order: tight leader seeds (PM_KNN_SEED)
-    monkeypatch.setenv("PM_KNN_SEED", seed)
+    q = q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))]   # spatial order
     for a, pa, b, pb in ((g, 1.0, c, 0.5), (c, 0.5, None, 0.0)):
         gm = pm_amd.PhotonMap(torch.from_numpy(a).cuda(), pa, None if b is None else torch.from_numpy(b).cuda(), pb)
         om = oracle.PhotonMap(a, pa, b, pb)

@@ -1,0 +1,137 @@
+"""GPU parity on the BASELINE workloads and the reference's own scenes (VERDICT
+r1 "what's missing" 4): the HIP path against the CPU oracle at the sizes the
+bench and the reference use, not only on toy cases.
+  - config 2 at FULL size: Cornell box, 1M diffuse + 1M caustic photons,
+    512x512, spp 1: photons bitwise, image within the north-star tolerance;
+  - config 3 reduced: the Sponza-class scene (266,912 triangles) with 1M + 100k
+    photons: photons bitwise, the k = 50 gather bitwise on 50k sampled queries,
+    a 240x135 image within tolerance;
+  - config 5 reduced: the caustics scene (square area light, glass) with a
+    k = 200 caustic gather, photons bitwise, image within tolerance;
+  - the reference's dragon-box.glb (91,226 triangles, one 1000 W light);
+  - the reference's default scene from config.toml.example (sphere.glb, its
+    camera / sky / depth / max_depth) at a reduced frame and spp.
+Tolerance (BASELINE north_star): L_inf <= 1e-3 per channel on the [0,1]-clamped
+colour, >= 99.9 % of pixels bitwise, render counters equal. The full-size
+config 3 frame is covered against the plain-walk library in
+test_gpu_check_variant.py (the oracle is too slow for 36M queries)."""
+import os
+
+import numpy as np
+import pytest
+
+import conftest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+NT = conftest.ORACLE_THREADS
+CAM = ((80.0, 30.0, 0.0), (10.0, 20.0, 0.0), (0.0, 1.0, 0.0), 0.87)
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _trace_pair(meshes, lights, casted, caustic, max_depth=10):
+    import oracle
+    import pm_amd
+    gs, os_ = pm_amd.Scene(meshes), oracle.Scene(meshes)
+    g = pm_amd.run_normal(gs, lights, casted, max_depth)
+    c = pm_amd.run_caustics(gs, lights, caustic, max_depth)
+    og = oracle.trace(os_, lights, casted, max_depth, False, nthreads=NT)
+    oc = oracle.trace(os_, lights, caustic, max_depth, True, nthreads=NT)
+    assert g.shape[0] == len(og) > 0 and c.shape[0] == len(oc)
+    assert np.array_equal(_bits(g.cpu().numpy()), _bits(og)), "global photons differ"
+    assert np.array_equal(_bits(c.cpu().numpy()), _bits(oc)), "caustic photons differ"
+    return gs, os_, g, c, og, oc
+
+
+def _render_check(gs, os_, lights, g, c, og, oc, W, H, spp=1, depth=30, sky=(1, 1, 1), cam=CAM, caustic_k=0):
+    import oracle
+    import pm_amd
+    gm, cm = pm_amd.load_photons(g, c)
+    camera = pm_amd.setup_camera(*cam, W, H)
+    ocam = oracle.camera_setup(*cam, W, H)
+    assert bytes(camera) == bytes(ocam)
+    rgba, rgb = pm_amd.render(gs, camera, W, H, spp, depth, sky, lights, gm, cm, caustic_k=caustic_k)
+    st = pm_amd.render_stats()
+    om_g = oracle.PhotonMap(og, 1.0, oc, 0.5, nthreads=NT)
+    om_c = oracle.PhotonMap(oc, 0.5, nthreads=NT)
+    orgba, orgb, ost = oracle.render(os_, ocam, W, H, spp, depth, sky, lights, om_g, om_c, nthreads=NT,
+                                     caustic_k=caustic_k)
+    assert (st.pixels, st.path_vertices, st.caustic_queries, st.global_queries, st.rays) == \
+        (ost.pixels, ost.path_vertices, ost.caustic_queries, ost.global_queries, ost.rays)
+    rgb = rgb.cpu().numpy()
+    err = float(np.abs(np.clip(rgb, 0, 1) - np.clip(orgb, 0, 1)).max())
+    exact = float(np.mean(np.all(_bits(rgb) == _bits(orgb), axis=-1)))
+    assert err <= 1e-3, err
+    assert exact >= 0.999, exact
+    assert np.mean(rgba.cpu().numpy().view(np.uint32) != orgba) <= 0.001
+    assert np.mean(orgb) > 0.01   # a lit image, not an all-black comparison
+    return gm, cm, om_g, om_c, st
+
+
+def test_config2_cornell_full_size(cornell):
+    """BASELINE config 2 exactly: Cornell, 1M + 1M photons, 512x512, spp 1."""
+    meshes, lights = cornell
+    gs, os_, g, c, og, oc = _trace_pair(meshes, lights, 1_000_000, 1_000_000)
+    _, _, _, _, st = _render_check(gs, os_, lights, g, c, og, oc, 512, 512)
+    assert st.pixels == 512 * 512 and st.global_queries > 1_000_000
+
+
+def test_config3_sponza_class_reduced():
+    """Config 3's scene and pipeline at 1M + 100k photons: gather bitwise on 50k
+    sampled queries in walk order (leader-seeded), image 240x135."""
+    import pm_amd
+    from pm_amd import scenes
+    meshes, lights = scenes.sponza_class()
+    assert sum(len(m.indices) for m in meshes) == 266_912
+    gs, os_, g, c, og, oc = _trace_pair(meshes, lights, 1_000_000, 100_000)
+    gm, cm, om_g, om_c, st = _render_check(gs, os_, lights, g, c, og, oc, 240, 135)
+    rng = np.random.default_rng(3)
+    q = og[rng.integers(0, len(og), 50_000), 0:3] + rng.normal(scale=0.3, size=(50_000, 3)).astype(np.float32)
+    q = np.ascontiguousarray(q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))].astype(np.float32))
+    brdf = rng.uniform(0, 0.4, size=len(q)).astype(np.float32)
+    qt, bt = torch.from_numpy(q).cuda(), torch.from_numpy(brdf).cuda()
+    for gpu_map, cpu_map in ((gm, om_g), (cm, om_c)):
+        got = pm_amd.gather_photons(gpu_map, qt, bt).cpu().numpy()
+        assert np.array_equal(_bits(got), _bits(cpu_map.gather(q, brdf, nthreads=NT)))
+
+
+def test_config5_caustics_reduced():
+    """Config 5's scene: square area light + glass/mirror spheres, caustic gather
+    over k = 200 (pm_render_params.caustic_k), photons bitwise, image 160x90."""
+    import pm_amd
+    from pm_amd import scenes
+    meshes, lights = scenes.sponza_caustics()
+    assert "normal" in lights[0]   # SQUARE_LIGHT
+    gs, os_, g, c, og, oc = _trace_pair(meshes, lights, 400_000, 600_000)
+    assert len(oc) > 10_000
+    _render_check(gs, os_, lights, g, c, og, oc, 160, 90, caustic_k=200)
+
+
+def test_reference_dragon_scene():
+    """The reference's dragon-box.glb (assets/models/dragon): glass dragon
+    (dragon-box.mtl), 91,226 triangles, one 1000 W light."""
+    import pm_amd
+    meshes, lights = pm_amd.load_scene_file(os.path.join(conftest.SCENES, "dragon", "dragon-box.glb"))
+    assert sum(len(m.indices) for m in meshes) == 91_226
+    gs, os_, g, c, og, oc = _trace_pair(meshes, lights, 1_000_000, 1_000_000)
+    assert len(oc) > 1000   # the glass dragon focuses caustic photons
+    _render_check(gs, os_, lights, g, c, og, oc, 160, 120)
+
+
+def test_reference_default_config_scene():
+    """config.toml.example as the reference ships it (sphere.glb, its camera,
+    sky, depth 30, max_depth 10), photon counts raised to 200k + 100k and the
+    frame reduced from 800x600 spp 24 to 200x150 spp 4."""
+    import pm_amd
+    cfg = pm_amd.load_config(os.path.join(conftest.GOLDEN, "config.toml.example"))
+    assert os.path.basename(cfg.model_path.decode()) == "sphere.glb"
+    assert (cfg.fb_width, cfg.fb_height, cfg.samples_per_pixel, cfg.depth) == (800, 600, 24, 30)
+    meshes, lights = pm_amd.load_scene_file(os.path.join(conftest.SCENES, "sphere", "sphere.glb"))
+    cam = (tuple(getattr(cfg.look_from, a) for a in "xyz"), tuple(getattr(cfg.look_at, a) for a in "xyz"),
+           tuple(getattr(cfg.look_up, a) for a in "xyz"), cfg.fovy)
+    sky = tuple(getattr(cfg.sky_colour, a) for a in "xyz")
+    gs, os_, g, c, og, oc = _trace_pair(meshes, lights, 200_000, 100_000, max_depth=cfg.max_depth)
+    _render_check(gs, os_, lights, g, c, og, oc, 200, 150, spp=4, depth=cfg.depth, sky=sky, cam=cam)
