@@ -195,6 +195,13 @@ def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libpm_hip.so not built at {LIB_PATH}: run `make -C photon-mapping_amd` "
                           "(or __graft_entry__.build()); the product has no CPU fallback")
+    # libpm_hip.so and torch both need libamdhip64.so.7 (one soname, two builds:
+    # /opt/rocm and torch's bundled copy); the first one loaded serves the whole
+    # process, and torch only finds the GPU with its own. Load torch first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in _SIGNATURES.items():
         fn = getattr(lib, name)

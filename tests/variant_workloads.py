@@ -147,6 +147,7 @@ def _digest(t):
 
 
 if __name__ == "__main__":
+    import torch  # noqa: F401  (torch's HIP runtime first: see pm_amd._load)
     import pm_amd
     print("library:", pm_amd.LIB_PATH, flush=True)
     res = run(full="--full" in sys.argv)
