@@ -1,0 +1,410 @@
+// knn_sim.c -- CPU cost model of the final-gather kNN walk (design tool, not
+// product, not a test): builds the left-balanced kd-tree of a photon cloud
+// (same split rules as kd_build), Morton-sorts a query cloud, and counts per
+// 64-query wave:
+//   A  the production per-lane walk (stack-free, post-order, JUMP, leader-
+//      seeded cut-offs): node loads per lane (mean) and per wave (max lane);
+//   B  a wave-uniform packet walk (one traversal per wave, a node is loaded
+//      once and tested by all 64 lanes; the far child is entered when ANY
+//      lane's ball crosses the plane): nodes per wave;
+//   C  B with subtrees of <= BUCKET nodes tested exhaustively (one vector
+//      load per bucket, every lane tests every point).
+// Inserts per lane (list updates) are counted for each.
+// Build: gcc -O2 -o /tmp/knn_sim tools/knn_sim.c -lm
+// Run:   /tmp/knn_sim pts.f32 queries.f32 [waves_to_sample]
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define K 50
+#define R2 1e4f
+#define STRIDE 16
+static int BUCKET = 63;
+
+typedef struct { float p[3]; int id, dim; } Node;
+static float* P;
+static Node* T;
+static int N;
+
+static int left_size(int s) {
+  if (s <= 1) return 0;
+  int h = 0;
+  while ((1 << h) <= s) h++;
+  const int half = 1 << (h - 2), full = (1 << (h - 1)) - 1, last = s - full;
+  return (half - 1) + (last < half ? last : half);
+}
+static int cmp_dim;
+static int less(int a, int b) {
+  const float ca = P[3 * a + cmp_dim], cb = P[3 * b + cmp_dim];
+  return ca < cb || (ca == cb && a < b);
+}
+static void select_k(int* v, int n, int k) {
+  int lo = 0, hi = n - 1;
+  while (hi > lo) {
+    int pv = v[lo + (hi - lo) / 2], i = lo, j = hi;
+    while (i <= j) {
+      while (less(v[i], pv)) i++;
+      while (less(pv, v[j])) j--;
+      if (i <= j) { int t = v[i]; v[i] = v[j]; v[j] = t; i++; j--; }
+    }
+    if (k <= j) hi = j; else if (k >= i) lo = i; else return;
+  }
+}
+static void build(int t, int* v, int s) {
+  if (s <= 0) return;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = 0; i < s; i++)
+    for (int d = 0; d < 3; d++) {
+      const float c = P[3 * v[i] + d];
+      if (c < mn[d]) mn[d] = c;
+      if (c > mx[d]) mx[d] = c;
+    }
+  int dim = 0;
+  if (mx[1] - mn[1] > mx[dim] - mn[dim]) dim = 1;
+  if (mx[2] - mn[2] > mx[dim] - mn[dim]) dim = 2;
+  const int ls = left_size(s);
+  cmp_dim = dim;
+  select_k(v, s, ls);
+  const int e = v[ls];
+  for (int d = 0; d < 3; d++) T[t].p[d] = P[3 * e + d];
+  T[t].id = e;
+  T[t].dim = dim;
+  build(2 * t + 1, v, ls);
+  build(2 * t + 2, v + ls + 1, s - ls - 1);
+}
+
+// ---- candidate list: the K smallest (d2, id) keys, kept sorted
+typedef struct { uint64_t key[K]; int n; } List;
+static uint64_t mkkey(float d2, int id) {
+  uint32_t b;
+  memcpy(&b, &d2, 4);
+  return (uint64_t)b << 32 | (uint32_t)id;
+}
+static float key_d2(uint64_t k) {
+  const uint32_t b = (uint32_t)(k >> 32);
+  float f;
+  memcpy(&f, &b, 4);
+  return f;
+}
+static void list_init(List* L) { L->n = 0; }
+static int list_insert(List* L, uint64_t k) {   // returns 1 if inserted
+  int n = L->n < K ? L->n : K - 1;
+  if (L->n >= K && !(k < L->key[K - 1])) return 0;
+  int j = n;
+  while (j > 0 && L->key[j - 1] > k) { L->key[j] = L->key[j - 1]; j--; }
+  L->key[j] = k;
+  if (L->n < K) L->n++;
+  return 1;
+}
+static float bound_of(const List* L, float cut) { return L->n < K ? cut : key_d2(L->key[K - 1]); }
+
+static float dist2(const float* q, const Node* nd) {
+  const float dx = q[0] - nd->p[0], dy = q[1] - nd->p[1], dz = q[2] - nd->p[2];
+  return dx * dx + dy * dy + dz * dz;
+}
+
+// ---- A: per-lane JUMP walk (lean_step), returns node loads; counts inserts
+static int walk_lane(const float* q, float cut, List* L, int* ins) {
+  list_init(L);
+  int prev = -1, curr = 0, depth = 0, steps = 0;
+  uint32_t far_mask = 0;
+  float bound = cut;
+  for (;;) {
+    const Node* nd = &T[curr];
+    steps++;
+    const int child = 2 * curr + 1;
+    const float diff = q[nd->dim] - nd->p[nd->dim];
+    const int side = diff > 0.f, close = child + side, far = child + 1 - side;
+    const int down = prev < child;
+    const int test = (down && close >= N) || prev == close;
+    if (test) {
+      const float d2 = dist2(q, nd);
+      if (d2 <= cut && list_insert(L, mkkey(d2, nd->id))) { (*ins)++; bound = bound_of(L, cut); }
+    }
+    int next, nprev;
+    if (down && close < N) {
+      next = close; nprev = curr; far_mask &= ~(2u << depth); depth++;
+    } else if (far < N && diff * diff <= bound) {
+      next = far; nprev = curr; far_mask |= 2u << depth; depth++;
+    } else {
+      const uint32_t open = (~far_mask & ((2u << depth) - 1u)) | 1u;
+      int da = 31;
+      while (!(open >> da & 1)) da--;
+      const int a = ((curr + 1) >> (depth - da)) - 1;
+      next = da == 0 ? -1 : ((a + 1) >> 1) - 1;
+      nprev = a;
+      depth = da - 1;
+    }
+    if (next < 0) break;
+    prev = nprev;
+    curr = next;
+  }
+  return steps;
+}
+
+// ---- B / C: wave-uniform packet walk
+typedef struct { const float* q[64]; float cut[64]; List L[64]; int n; long nodes, buckets, bucket_pts, ins; int lins[64]; } Packet;
+static int subtree_size(int t) {   // nodes of the implicit subtree of t
+  int s = 0;
+  for (long lo = t, hi = t; lo < N; lo = 2 * lo + 1, hi = 2 * hi + 2) s += (int)((hi < N ? hi : N - 1) - lo + 1);
+  return s;
+}
+static void packet_test(Packet* W, const Node* nd) {
+  for (int l = 0; l < W->n; l++) {
+    const float d2 = dist2(W->q[l], nd);
+    if (d2 <= W->cut[l] && list_insert(&W->L[l], mkkey(d2, nd->id))) { W->ins++; W->lins[l]++; }
+  }
+}
+static int lane_needs(Packet* W, int l, const Node* nd, int side_of_child) {
+  const float diff = W->q[l][nd->dim] - nd->p[nd->dim];
+  const int side = diff > 0.f;
+  if (side == side_of_child) return 1;
+  return diff * diff <= bound_of(&W->L[l], W->cut[l]);
+}
+static void packet_visit(Packet* W, int t, int bucket) {
+  if (t >= N) return;
+  if (bucket && subtree_size(t) <= BUCKET) {   // C: exhaustive bucket
+    W->buckets++;
+    for (long lo = t, hi = t; lo < N; lo = 2 * lo + 1, hi = 2 * hi + 2)
+      for (long u = lo; u <= hi && u < N; u++) { packet_test(W, &T[u]); W->bucket_pts++; }
+    return;
+  }
+  W->nodes++;
+  const Node* nd = &T[t];
+  int votes = 0;
+  for (int l = 0; l < W->n; l++) votes += (W->q[l][nd->dim] - nd->p[nd->dim]) > 0.f;
+  const int first = votes * 2 > W->n ? 1 : 0;
+  int need = 0;
+  for (int l = 0; l < W->n && !need; l++) need = lane_needs(W, l, nd, first);
+  if (need) packet_visit(W, 2 * t + 1 + first, bucket);
+  packet_test(W, nd);   // post-order (after the majority's close child)
+  need = 0;
+  for (int l = 0; l < W->n && !need; l++) need = lane_needs(W, l, nd, 1 - first);
+  if (need) packet_visit(W, 2 * t + 2 - first, bucket);
+}
+
+
+// ---- D: lockstep wave model of the production loop (lean_step + LDS queue of
+// QL keys). Every iteration advances every walking lane by one node; a round
+// runs when some lane's queue is full or no lane walks. policy 0: each lane pops
+// ONE queued key (production); policy 1: each lane merges ALL its queued keys.
+// Returns iterations; *rounds = insert rounds.
+static int QL = 8;
+typedef struct {
+  const float* q; float cut, bound; List L; int prev, curr, depth, walking, qn; uint32_t far_mask; uint64_t qk[32];
+} Lane;
+static int wave_lockstep(const float* const* qs, const float* cuts, int policy, int* rounds, long* lane_ins) {
+  Lane ln[64];
+  for (int l = 0; l < 64; l++) {
+    ln[l].q = qs[l]; ln[l].cut = cuts[l]; ln[l].bound = cuts[l]; list_init(&ln[l].L);
+    ln[l].prev = -1; ln[l].curr = 0; ln[l].depth = 0; ln[l].walking = 1; ln[l].qn = 0; ln[l].far_mask = 0;
+  }
+  int it = 0;
+  *rounds = 0;
+  for (;;) {
+    it++;
+    int any_walk = 0, any_full = 0;
+    for (int l = 0; l < 64; l++) {
+      Lane* w = &ln[l];
+      if (!w->walking) continue;
+      const Node* nd = &T[w->curr];
+      const int child = 2 * w->curr + 1;
+      const float diff = w->q[nd->dim] - nd->p[nd->dim];
+      const int side = diff > 0.f, close = child + side, far = child + 1 - side;
+      const int down = w->prev < child;
+      if ((down && close >= N) || w->prev == close) {
+        const float d2 = dist2(w->q, nd);
+        const uint64_t k = mkkey(d2, nd->id);
+        const int full = w->L.n >= K;
+        if (d2 <= w->cut && (!full || k < w->L.key[K - 1])) w->qk[w->qn++] = k;
+      }
+      int next, nprev;
+      if (down && close < N) {
+        next = close; nprev = w->curr; w->far_mask &= ~(2u << w->depth); w->depth++;
+      } else if (far < N && diff * diff <= w->bound) {
+        next = far; nprev = w->curr; w->far_mask |= 2u << w->depth; w->depth++;
+      } else {
+        const uint32_t open = (~w->far_mask & ((2u << w->depth) - 1u)) | 1u;
+        int da = 31;
+        while (!(open >> da & 1)) da--;
+        const int a = ((w->curr + 1) >> (w->depth - da)) - 1;
+        next = da == 0 ? -1 : ((a + 1) >> 1) - 1;
+        nprev = a;
+        w->depth = da - 1;
+      }
+      if (next < 0) w->walking = 0; else { w->prev = nprev; w->curr = next; }
+    }
+    for (int l = 0; l < 64; l++) { any_walk |= ln[l].walking; any_full |= ln[l].qn == QL; }
+    if (any_full || !any_walk) {
+      (*rounds)++;
+      int left = 0;
+      for (int l = 0; l < 64; l++) {
+        Lane* w = &ln[l];
+        const int take = policy ? w->qn : (w->qn > 0);
+        for (int t = 0; t < take; t++) {
+          const uint64_t k = w->qk[--w->qn];
+          if (list_insert(&w->L, k)) (*lane_ins)++;
+        }
+        w->bound = bound_of(&w->L, w->cut);
+        left |= w->qn > 0;
+      }
+      if (!any_walk && !left) break;
+    }
+  }
+  return it;
+}
+
+static uint32_t part1by2(uint32_t x) {
+  x &= 0x3FF;
+  x = (x | (x << 16)) & 0x30000FF; x = (x | (x << 8)) & 0x300F00F;
+  x = (x | (x << 4)) & 0x30C30C3; x = (x | (x << 2)) & 0x9249249;
+  return x;
+}
+static uint64_t* MK;
+static int cmp_mk(const void* a, const void* b) {
+  const uint64_t x = MK[*(const int*)a], y = MK[*(const int*)b];
+  return x < y ? -1 : x > y;
+}
+static double seed_bound(const float* lq, float lt, const float* q) {
+  if (lt < 0) return 1e300;
+  const double dx = (double)q[0] - lq[0], dy = (double)q[1] - lq[1], dz = (double)q[2] - lq[2];
+  const double c = (sqrt((double)lt) + sqrt(dx * dx + dy * dy + dz * dz)) * (1.0 + 1e-6);
+  return c * c * (1.0 + 1e-5) + 1e-30;
+}
+
+static float* readf(const char* path, long* n) {
+  FILE* f = fopen(path, "rb");
+  if (!f) { perror(path); exit(1); }
+  fseek(f, 0, SEEK_END);
+  *n = ftell(f) / 12;
+  fseek(f, 0, SEEK_SET);
+  float* a = malloc((size_t)*n * 12);
+  if (fread(a, 12, (size_t)*n, f) != (size_t)*n) exit(1);
+  fclose(f);
+  return a;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) { fprintf(stderr, "usage: %s pts.f32 qs.f32 [waves]\n", argv[0]); return 1; }
+  long np, nq;
+  P = readf(argv[1], &np);
+  float* Q = readf(argv[2], &nq);
+  const int sample = argc > 3 ? atoi(argv[3]) : 2000;
+  if (argc > 4) BUCKET = atoi(argv[4]);
+  if (argc > 5) QL = atoi(argv[5]);
+  N = (int)np;
+  T = malloc(sizeof(Node) * (size_t)N);
+  int* v = malloc(sizeof(int) * (size_t)N);
+  for (int i = 0; i < N; i++) v[i] = i;
+  build(0, v, N);
+  // Morton order of the queries over their bounds (30-bit)
+  float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (long i = 0; i < nq; i++)
+    for (int d = 0; d < 3; d++) { lo[d] = fminf(lo[d], Q[3 * i + d]); hi[d] = fmaxf(hi[d], Q[3 * i + d]); }
+  MK = malloc(8 * (size_t)nq);
+  int* ord = malloc(sizeof(int) * (size_t)nq);
+  for (long i = 0; i < nq; i++) {
+    uint32_t c[3];
+    for (int d = 0; d < 3; d++) {
+      float u = (Q[3 * i + d] - lo[d]) / (hi[d] - lo[d]);
+      c[d] = (uint32_t)fminf(fmaxf(u * 1024.f, 0.f), 1023.f);
+    }
+    MK[i] = ((uint64_t)(part1by2(c[0]) << 2 | part1by2(c[1]) << 1 | part1by2(c[2])) << 32) | (uint64_t)i;
+    ord[i] = (int)i;
+  }
+  qsort(ord, (size_t)nq, sizeof(int), cmp_mk);
+  const long nwaves = nq / 64;
+  // leader records (every STRIDE-th query in walk order, plain cut-off)
+  const long nl = (nq + STRIDE - 1) / STRIDE;
+  float* lt = malloc(sizeof(float) * (size_t)nl);
+  List L;
+  int dummy = 0;
+  srand(12345);
+  long* waves = malloc(sizeof(long) * (size_t)sample);
+  for (int s = 0; s < sample; s++) waves[s] = (long)((double)rand() / RAND_MAX * (nwaves - 1));
+  // only the leaders the sampled waves consult are walked
+  char* need = calloc((size_t)nl, 1);
+  for (int s = 0; s < sample; s++) {
+    const long r0 = waves[s] * 64;
+    for (long r = r0 - 2 * STRIDE; r < r0 + 64 + 3 * STRIDE; r += STRIDE)
+      if (r >= 0 && r / STRIDE < nl) need[r / STRIDE] = 1;
+  }
+  for (long j = 0; j < nl; j++) {
+    if (!need[j]) continue;
+    walk_lane(&Q[3 * ord[j * STRIDE]], nextafterf(R2, 0.f), &L, &dummy);
+    lt[j] = L.n >= K ? key_d2(L.key[K - 1]) : -1.f;
+  }
+  double a_mean = 0, a_max = 0, a_ins = 0, b_nodes = 0, b_ins = 0, c_nodes = 0, c_buckets = 0, c_pts = 0, c_ins = 0;
+  double a_plain_max = 0, b_plain = 0, c_maxins = 0, b_maxins = 0, d_it[2] = {0, 0}, d_rounds[2] = {0, 0}, d_ins[2] = {0, 0};
+  for (int s = 0; s < sample; s++) {
+    const long r0 = waves[s] * 64;
+    Packet W, Wp, Wc;
+    memset(&W, 0, sizeof(W));
+    int mx = 0, mxp = 0, ins = 0;
+    for (int l = 0; l < 64; l++) {
+      const long r = r0 + l;
+      const float* q = &Q[3 * ord[r]];
+      float cut = nextafterf(R2, 0.f);
+      if (r % STRIDE) {
+        const long jp = r / STRIDE;
+        double b = 1e300;
+        for (long j = jp - 1; j <= jp + 2; j++)
+          if (j >= 0 && j < nl) b = fmin(b, seed_bound(&Q[3 * ord[j * STRIDE]], lt[j], q));
+        if (b < cut) cut = (float)b * (1.f + 1e-7f);
+      }
+      const int st = walk_lane(q, cut, &L, &ins);
+      a_mean += st;
+      if (st > mx) mx = st;
+      int d2 = 0;
+      const int sp = walk_lane(q, nextafterf(R2, 0.f), &L, &d2);
+      if (sp > mxp) mxp = sp;
+      W.q[l] = q;
+      W.cut[l] = cut;
+    }
+    W.n = 64;
+    for (int pol = 0; pol < 2; pol++) {
+      int rounds = 0;
+      long li = 0;
+      d_it[pol] += wave_lockstep(W.q, W.cut, pol, &rounds, &li);
+      d_rounds[pol] += rounds;
+      d_ins[pol] += li;
+    }
+    a_max += mx;
+    a_plain_max += mxp;
+    a_ins += ins;
+    Wp = W;
+    for (int l = 0; l < 64; l++) { list_init(&W.L[l]); Wp.cut[l] = nextafterf(R2, 0.f); list_init(&Wp.L[l]); }
+    Wc = W;
+    packet_visit(&W, 0, 0);
+    b_nodes += W.nodes;
+    b_ins += W.ins;
+    packet_visit(&Wp, 0, 0);
+    b_plain += Wp.nodes;
+    packet_visit(&Wc, 0, 1);
+    c_nodes += Wc.nodes;
+    c_buckets += Wc.buckets;
+    c_pts += Wc.bucket_pts;
+    c_ins += Wc.ins;
+    int m = 0;
+    for (int l = 0; l < 64; l++) m = Wc.lins[l] > m ? Wc.lins[l] : m;
+    c_maxins += m;
+    m = 0;
+    for (int l = 0; l < 64; l++) m = W.lins[l] > m ? W.lins[l] : m;
+    b_maxins += m;
+  }
+  const double S = sample;
+  printf("photons %d queries %ld waves %ld (sampled %d)\n", N, nq, nwaves, sample);
+  printf("A per-lane JUMP walk, seeded: loads/lane %.1f, wave max %.1f (plain cut: wave max %.1f), inserts/lane %.1f\n",
+         a_mean / S / 64, a_max / S, a_plain_max / S, a_ins / S / 64);
+  printf("B packet walk, seeded: nodes/wave %.1f (plain cut %.1f), inserts/lane %.1f (max lane %.1f)\n", b_nodes / S,
+         b_plain / S, b_ins / S / 64, b_maxins / S);
+  printf("C packet + %d-node buckets: nodes/wave %.1f, buckets/wave %.1f (%.0f points), inserts/lane %.1f (max lane %.1f)\n",
+         BUCKET, c_nodes / S, c_buckets / S, c_pts / S, c_ins / S / 64, c_maxins / S);
+  for (int pol = 0; pol < 2; pol++)
+    printf("D lockstep wave (QL %d, %s rounds): iterations %.1f, rounds %.1f, inserts/lane %.1f\n", QL,
+           pol ? "batch-merge" : "pop-one", d_it[pol] / S, d_rounds[pol] / S, d_ins[pol] / S / 64);
+  return 0;
+}
