@@ -9,10 +9,16 @@
 // Algorithm (presorted lists, level by level): the points are sorted once per
 // dimension (stable radix sort on (coord, index)); every level then splits each
 // active subtree range at its left-balanced median — the median element is read
-// directly from the list of the chosen dimension and the three lists are
-// stably partitioned around it (segmented count scan over 1024-position tiles:
-// k_kd_count -> k_kd_chunkscan / k_kd_chunkcarry -> k_kd_part). Subtree ranges are identical in the three lists, so a single tag
-// array tracks subtree membership. Ties are broken by the original index.
+// directly from the list of the chosen dimension and the two OTHER lists are
+// stably partitioned around it (segmented count scan over 512-position tiles:
+// k_kd_count -> k_kd_chunkscan / k_kd_chunkcarry -> k_kd_part). The split
+// dimension's own list is already partitioned (it is sorted on that dimension)
+// and is not moved: every list has two buffers and each subtree records which
+// buffer holds each of its three lists (SegTab::sel). The lists are SoA (x, y,
+// z, original index as four arrays), so the count pass reads only the split
+// coordinate (and the index on a coordinate tie). Subtree ranges are identical
+// in the three lists, so a single tag array tracks subtree membership. Ties are
+// broken by the original index.
 #include <algorithm>
 
 #include "pm_internal.hpp"
@@ -38,10 +44,27 @@ __global__ void k_kd_init_keys(const float4* elems, int64_t n, int d, uint32_t* 
   vals[i] = (uint32_t)i;
 }
 
-__global__ void k_kd_gather(const float4* elems, const uint32_t* order, int64_t n, float4* out) {
+// The presorted lists: list d (sorted on dimension d) in buffer k (0 / 1) as
+// four arrays (x, y, z, original index bits), one allocation of 24 n floats.
+struct KdLists {
+  float* base;
+  int64_t n;
+  __host__ __device__ float* comp(int d, int k, int c) const { return base + (int64_t)((d * 2 + k) * 4 + c) * n; }
+};
+
+__global__ void k_kd_gather_soa(const float4* __restrict__ elems, const uint32_t* __restrict__ order, int64_t n,
+                                KdLists Lst, int d) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  out[i] = elems[order[i]];
+  const float4 e = elems[order[i]];
+  Lst.comp(d, 0, 0)[i] = e.x;
+  Lst.comp(d, 0, 1)[i] = e.y;
+  Lst.comp(d, 0, 2)[i] = e.z;
+  Lst.comp(d, 0, 3)[i] = e.w;
+}
+
+__device__ __forceinline__ float4 kd_elem(const KdLists& Lst, int d, int k, int64_t p) {
+  return make_float4(Lst.comp(d, k, 0)[p], Lst.comp(d, k, 1)[p], Lst.comp(d, k, 2)[p], Lst.comp(d, k, 3)[p]);
 }
 
 struct SegTab {
@@ -51,33 +74,36 @@ struct SegTab {
   int32_t* dim;
   float* coord;
   int32_t* id;
+  int32_t* sel;   // bit d: buffer of list d for this subtree
 };
 
-__global__ void k_kd_seg(const float4* l0, const float4* l1, const float4* l2, int level, int64_t cap, SegTab T,
-                         float4* out_nodes) {
+__global__ void k_kd_seg(KdLists Lst, int level, int64_t cap, SegTab T, float4* out_nodes) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nseg = 1ll << level;
   if (j >= nseg) return;
   const int64_t t = nseg - 1 + j;
   const int b = T.b[t], s = T.s[t];
+  const int sel = T.sel[t];
   const int64_t c1 = 2 * t + 1, c2 = 2 * t + 2;
   if (s <= 0) {
     T.ls[t] = -1;
     if (c2 < cap) {
-      T.b[c1] = b; T.s[c1] = 0;
-      T.b[c2] = b; T.s[c2] = 0;
+      T.b[c1] = b; T.s[c1] = 0; T.sel[c1] = sel;
+      T.b[c2] = b; T.s[c2] = 0; T.sel[c2] = sel;
     }
     return;
   }
   const int ls = left_size(s);
-  const float4* L[3] = {l0, l1, l2};
   float ext[3];
 #pragma unroll
-  for (int d = 0; d < 3; d++) ext[d] = coord_of(L[d][b + s - 1], d) - coord_of(L[d][b], d);
+  for (int d = 0; d < 3; d++) {
+    const float* c = Lst.comp(d, (sel >> d) & 1, d);
+    ext[d] = c[b + s - 1] - c[b];
+  }
   int dim = 0;
   if (ext[1] > ext[dim]) dim = 1;
   if (ext[2] > ext[dim]) dim = 2;
-  const float4 e = L[dim][b + ls];
+  const float4 e = kd_elem(Lst, dim, (sel >> dim) & 1, b + ls);
   const int id = __float_as_int(e.w);
   T.ls[t] = ls;
   T.dim[t] = dim;
@@ -85,8 +111,10 @@ __global__ void k_kd_seg(const float4* l0, const float4* l1, const float4* l2, i
   T.id[t] = id;
   out_nodes[t] = make_float4(e.x, e.y, e.z, __int_as_float((id << 2) | dim));
   if (c2 < cap) {
-    T.b[c1] = b; T.s[c1] = ls;
-    T.b[c2] = b + ls + 1; T.s[c2] = s - ls - 1;
+    // the two non-split lists move to the other buffer this level
+    const int csel = sel ^ (7 ^ (1 << dim));
+    T.b[c1] = b; T.s[c1] = ls; T.sel[c1] = csel;
+    T.b[c2] = b + ls + 1; T.s[c2] = s - ls - 1; T.sel[c2] = csel;
   }
 }
 
@@ -100,19 +128,22 @@ __device__ __forceinline__ int kd_class(const float4 e, int dim, float nc, int n
 }
 
 // ------------------------------------------------------------------ partition
-// Per level (replaces flags -> u64 scan -> scatter -> tag): positions are cut
-// into 1024-position tiles; the element at each position of the three lists is
-// classed against its segment's median (L / M / R / already placed) and the
-// packed (L, R) counts are scanned SEGMENTED (reset at segment starts):
-//   k_kd_count     per-tile segmented aggregate,
+// Per level: positions are cut into 512-position tiles; the element at each
+// position of the two non-split lists is classed against its segment's median
+// (L / M / R; the split list and placed positions: 3) and the packed (L, R)
+// counts are scanned SEGMENTED (reset at segment starts):
+//   k_kd_count     per-tile segmented aggregate (reads the split coordinate,
+//                  the index only on a coordinate tie),
 //   k_kd_chunkscan / k_kd_chunkcarry  exclusive segmented carry per tile,
-//   k_kd_part      block scan + carry -> stable scatter: L -> b + #L before it
-//                  in the segment, M -> b + ls, R -> b + ls + 1 + #R before it;
-//                  the tag (segment id per position) is updated in place.
+//   k_kd_part      block scan + carry -> stable scatter into the other buffer:
+//                  L -> b + #L before it in the segment, M -> b + ls,
+//                  R -> b + ls + 1 + #R before it; the tag (segment id per
+//                  position) is updated in place.
 // Kernel boundaries order the passes (a decoupled look-back needs agent-scope
 // release fences per tile, i.e. L2 write-backs across the 8 XCDs: measured
-// 7 ms per level). Traffic per element and level: 2 x (3 x 16 B + 4 B) read,
-// 3 x 16 B + 4 B written.
+// 7 ms per level). Traffic per element and level: count 2 x 4 B + tag, part
+// 2 x 16 B read + 2 x 16 B written + tag read / write (84 B; the AoS lists that
+// moved all three 16-B lists took 140 B).
 // Occupancy targets (waves per SIMD, 0 = compiler's choice), build-time A/B knobs.
 #ifndef PM_KD_PART_WAVES
 #define PM_KD_PART_WAVES 0
@@ -121,9 +152,8 @@ __device__ __forceinline__ int kd_class(const float4 e, int dim, float nc, int n
 #define PM_KD_COUNT_WAVES 0
 #endif
 constexpr int kPartThreads = 256;
-// positions per thread (tile = 256 * IPT). Config 3 kd build: IPT 4 44.5 ms
-// (count 114 / part 142 VGPRs), IPT 2 36.4 ms (58 / 92), IPT 1 36.6 ms; forcing
-// occupancy at IPT 4 spills (49-62 ms)
+// positions per thread (tile = 256 * IPT). Config 3 kd build (AoS lists, round
+// 1): IPT 4 44.5 ms (count 114 / part 142 VGPRs), IPT 2 36.4 ms (58 / 92), IPT 1 36.6 ms
 #ifndef PM_KD_IPT
 #define PM_KD_IPT 2
 #endif
@@ -184,29 +214,31 @@ __device__ __forceinline__ SegVal block_seg_scan(const SegVal& th, SegVal* sh, S
   return seg_combine(wpre, ex);
 }
 
-// Striped tiles: item k of thread i sits at position tile*1024 + k*256 + i, so
-// every list load / scatter store of a wave covers 1 KB of consecutive
-// positions; the segmented scan runs once per k-round, carried across rounds.
+// Striped tiles: item k of thread i sits at position tile*512 + k*256 + i, so
+// every wave access covers 64 consecutive positions; the segmented scan runs
+// once per k-round, carried across rounds.
 struct PartItem {
-  int tg, sb, sls;
-  uint8_t cls[3];   // 0 L, 1 M, 2 R, 3 placed / out of range
+  int tg, sb, sls, sel;
+  uint8_t cls[3];   // 0 L, 1 M, 2 R, 3 not moved (split list / placed / out of range)
 };
 
+// Classes of position p in the three lists; KEEP: also load the moved
+// elements (into e[d]). The split list is never loaded (positional).
 template <bool KEEP>
-__device__ __forceinline__ SegVal part_load(const float4* __restrict__ l0, const float4* __restrict__ l1,
-                                            const float4* __restrict__ l2, const int32_t* __restrict__ tag,
-                                            int64_t n, const SegTab& T, int64_t p, PartItem& it, float4 (&e)[3]) {
-  const float4* L[3] = {l0, l1, l2};
+__device__ __forceinline__ SegVal part_load(const KdLists& Lst, const int32_t* __restrict__ tag, int64_t n,
+                                            const SegTab& T, int64_t p, PartItem& it, float4 (&e)[3]) {
   SegVal th = seg_zero();
   it.tg = p < n ? tag[p] : -1;
   int dim = 0, nid = 0;
   float nc = 0.f;
   it.sb = 0;
   it.sls = 0;
+  it.sel = 0;
   if (it.tg >= 0) {
     const int t = it.tg;
     it.sb = T.b[t];
     it.sls = T.ls[t];
+    it.sel = T.sel[t];
     dim = T.dim[t];
     nc = T.coord[t];
     nid = T.id[t];
@@ -214,22 +246,31 @@ __device__ __forceinline__ SegVal part_load(const float4* __restrict__ l0, const
   th.f = it.tg >= 0 && p == it.sb;
 #pragma unroll
   for (int d = 0; d < 3; d++) {
-    // the segment's own split-dimension list is sorted on that dimension, so
-    // its classes are positional: the count pass does not load it
-    const bool positional = it.tg >= 0 && d == dim;
-    const float4 x = (p < n && (KEEP || !positional)) ? L[d][p] : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (KEEP) e[d] = x;
-    const int64_t mid = (int64_t)it.sb + it.sls;
-    const int c = it.tg < 0 ? 3 : (positional ? (p < mid ? 0 : (p == mid ? 1 : 2)) : kd_class(x, dim, nc, nid));
+    int c = 3;
+    if (it.tg >= 0 && d != dim) {
+      const int k = (it.sel >> d) & 1;
+      if (KEEP) {
+        e[d] = kd_elem(Lst, d, k, p);
+        c = kd_class(e[d], dim, nc, nid);
+      } else {
+        // count pass: the split coordinate alone decides unless it ties the
+        // median's (then the index does; the median itself has c == nc)
+        const float cv = Lst.comp(d, k, dim)[p];
+        if (cv < nc) c = 0;
+        else if (cv > nc) c = 2;
+        else {
+          const int id = __float_as_int(Lst.comp(d, k, 3)[p]);
+          c = id < nid ? 0 : (id == nid ? 1 : 2);
+        }
+      }
+    }
     it.cls[d] = (uint8_t)c;
     th.v[d] = c == 0 ? 1ull : (c == 2 ? (1ull << 32) : 0ull);
   }
   return th;
 }
 
-__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void k_kd_count(const float4* __restrict__ l0,
-                                                           const float4* __restrict__ l1,
-                                                           const float4* __restrict__ l2,
+__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void k_kd_count(KdLists Lst,
                                                            const int32_t* __restrict__ tag, int64_t n, SegTab T,
                                                            SegVal* __restrict__ tile_agg) {
   __shared__ SegVal sh[kPartThreads / 64];
@@ -239,7 +280,7 @@ __global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void
 #pragma unroll
   for (int k = 0; k < kPartIPT; k++) {
     PartItem it;
-    th[k] = part_load<false>(l0, l1, l2, tag, n, T, base + k * kPartThreads, it, dummy);
+    th[k] = part_load<false>(Lst, tag, n, T, base + k * kPartThreads, it, dummy);
   }
   SegVal agg = seg_zero();
 #pragma unroll
@@ -281,21 +322,17 @@ __global__ __launch_bounds__(kChunk) void k_kd_chunkcarry(SegVal* __restrict__ c
   }
 }
 
-__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void k_kd_part(const float4* __restrict__ l0, const float4* __restrict__ l1,
-                                                          const float4* __restrict__ l2, float4* __restrict__ o0,
-                                                          float4* __restrict__ o1, float4* __restrict__ o2,
+__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void k_kd_part(KdLists Lst,
                                                           int32_t* __restrict__ tag, int64_t n, SegTab T,
                                                           const SegVal* __restrict__ tile_carry,
                                                           const SegVal* __restrict__ chunk_carry) {
   __shared__ SegVal sh[kPartThreads / 64];
   const int64_t base = (int64_t)blockIdx.x * kPartTile + threadIdx.x;
-  float4* O[3] = {o0, o1, o2};
   PartItem it[kPartIPT];
   float4 e[kPartIPT][3];
   SegVal th[kPartIPT];
 #pragma unroll
-  for (int k = 0; k < kPartIPT; k++)
-    th[k] = part_load<true>(l0, l1, l2, tag, n, T, base + k * kPartThreads, it[k], e[k]);
+  for (int k = 0; k < kPartIPT; k++) th[k] = part_load<true>(Lst, tag, n, T, base + k * kPartThreads, it[k], e[k]);
   SegVal carry = seg_combine(chunk_carry[blockIdx.x / kChunk], tile_carry[blockIdx.x]);
 #pragma unroll
   for (int k = 0; k < kPartIPT; k++) {
@@ -309,12 +346,16 @@ __global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void 
 #pragma unroll
     for (int d = 0; d < 3; d++) {
       const int c = it[k].cls[d];
+      if (c == 3) continue;
       int64_t dst;
-      if (c == 3) dst = p;
-      else if (c == 0) dst = it[k].sb + (int64_t)(uint32_t)run.v[d];
+      if (c == 0) dst = it[k].sb + (int64_t)(uint32_t)run.v[d];
       else if (c == 1) dst = it[k].sb + it[k].sls;
       else dst = it[k].sb + it[k].sls + 1 + (int64_t)(uint32_t)(run.v[d] >> 32);
-      O[d][dst] = e[k][d];
+      const int ko = ((it[k].sel >> d) & 1) ^ 1;
+      Lst.comp(d, ko, 0)[dst] = e[k][d].x;
+      Lst.comp(d, ko, 1)[dst] = e[k][d].y;
+      Lst.comp(d, ko, 2)[dst] = e[k][d].z;
+      Lst.comp(d, ko, 3)[dst] = e[k][d].w;
     }
     if (it[k].tg >= 0) {
       const int t = it[k].tg;
@@ -340,9 +381,9 @@ constexpr int kLocal = 1024;
 constexpr int kLocalWaveLevel = 4;
 static_assert(kLocal / 64 == (1 << kLocalWaveLevel), "one wave per level-4 sub-segment");
 
-__global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_kd_local(const float4* __restrict__ l0, const float4* __restrict__ l1,
-                                                     const float4* __restrict__ l2, int L0, SegTab T,
-                                                     float4* __restrict__ nodes) {
+__global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_kd_local(KdLists Lst, int L0,
+                                                                                           SegTab T,
+                                                                                           float4* __restrict__ nodes) {
   __shared__ float4 buf[3][kLocal];
   __shared__ int16_t tag[kLocal];
   __shared__ int16_t sb[2][kLocal / 2], ss[2][kLocal / 2];   // sub-segment start / size, ping-pong by level
@@ -356,10 +397,10 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
   const int64_t t = ((int64_t)1 << L0) - 1 + blockIdx.x;
   const int B = T.b[t], S = T.s[t];
   if (S <= 0) return;
-  const float4* L[3] = {l0, l1, l2};
+  const int sel = T.sel[t];
   if (tid < S) {
 #pragma unroll
-    for (int d = 0; d < 3; d++) buf[d][tid] = L[d][B + tid];
+    for (int d = 0; d < 3; d++) buf[d][tid] = kd_elem(Lst, d, (sel >> d) & 1, B + tid);
   }
   tag[tid] = tid < S ? 0 : -1;
   stage[tid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
@@ -529,12 +570,9 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
   int H = 0;
   while ((1ll << H) <= n) H++;          // levels = floor(log2 n) + 1
   const int64_t cap = 1ll << (H + 1);
-  DevBuf<float4> la[3], lb[3];
-  for (int d = 0; d < 3; d++) {
-    la[d].alloc(n);
-    lb[d].alloc(n);
-    if (!la[d].p || !lb[d].p) return hipErrorOutOfMemory;
-  }
+  DevBuf<float> lists((size_t)24 * n);
+  if (!lists.p) return hipErrorOutOfMemory;
+  const KdLists Lst{lists.p, n};
   {
     DevBuf<uint32_t> keys(n), vals(n);
     if (!keys.p || !vals.p) return hipErrorOutOfMemory;
@@ -542,51 +580,45 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
       k_kd_init_keys<<<grid_for(n, 256), 256, 0, s>>>(elems, n, d, keys.p, vals.p);
       PM_HIP_TRY(hipGetLastError());
       PM_HIP_TRY(radix_sort_pairs(keys.p, vals.p, n, 32, s));
-      k_kd_gather<<<grid_for(n, 256), 256, 0, s>>>(elems, vals.p, n, la[d].p);
+      k_kd_gather_soa<<<grid_for(n, 256), 256, 0, s>>>(elems, vals.p, n, Lst, d);
       PM_HIP_TRY(hipGetLastError());
     }
   }
-  DevBuf<int32_t> tb(cap), ts(cap), tls(cap), tdim(cap), tid(cap), tag(n);
+  DevBuf<int32_t> tb(cap), ts(cap), tls(cap), tdim(cap), tid(cap), tsel(cap), tag(n);
   DevBuf<float> tco(cap);
   const int64_t ntiles = (n + kPartTile - 1) / kPartTile;
   const int nchunks = (int)((ntiles + kChunk - 1) / kChunk);
   DevBuf<SegVal> tagg(ntiles), tcarry(ntiles), ccarry(nchunks);
-  if (!tb.p || !ts.p || !tls.p || !tdim.p || !tid.p || !tag.p || !tco.p || !tagg.p || !tcarry.p || !ccarry.p)
+  if (!tb.p || !ts.p || !tls.p || !tdim.p || !tid.p || !tsel.p || !tag.p || !tco.p || !tagg.p || !tcarry.p ||
+      !ccarry.p)
     return hipErrorOutOfMemory;
-  SegTab T{tb.p, ts.p, tls.p, tdim.p, tco.p, tid.p};
-  const int32_t root[2] = {0, (int32_t)n};
+  SegTab T{tb.p, ts.p, tls.p, tdim.p, tco.p, tid.p, tsel.p};
+  const int32_t root[3] = {0, (int32_t)n, 0};
   PM_HIP_TRY(hipMemcpyAsync(tb.p, &root[0], 4, hipMemcpyHostToDevice, s));
   PM_HIP_TRY(hipMemcpyAsync(ts.p, &root[1], 4, hipMemcpyHostToDevice, s));
+  PM_HIP_TRY(hipMemcpyAsync(tsel.p, &root[2], 4, hipMemcpyHostToDevice, s));
   PM_HIP_TRY(hipMemsetAsync(tag.p, 0, sizeof(int32_t) * n, s));
-  float4* cur[3] = {la[0].p, la[1].p, la[2].p};
-  float4* nxt[3] = {lb[0].p, lb[1].p, lb[2].p};
   // segments at L0 hold <= 1023 elements; the check variant keeps every level
   // global (the identical-tree test compares the two libraries)
   const int L0 = PM_CHECK_VARIANT ? H : std::max(0, H - 10);
   for (int L = 0; L < H; L++) {
     if (L == L0) {
-      k_kd_local<<<(int)(1ll << L0), kLocal, 0, s>>>(cur[0], cur[1], cur[2], L0, T, nodes);
+      k_kd_local<<<(int)(1ll << L0), kLocal, 0, s>>>(Lst, L0, T, nodes);
       PM_HIP_TRY(hipGetLastError());
       break;
     }
     const int64_t nseg = 1ll << L;
-    k_kd_seg<<<grid_for(nseg, 256), 256, 0, s>>>(cur[0], cur[1], cur[2], L, cap, T, nodes);
+    k_kd_seg<<<grid_for(nseg, 256), 256, 0, s>>>(Lst, L, cap, T, nodes);
     PM_HIP_TRY(hipGetLastError());
     if (L == H - 1) break;   // last level: every remaining subtree has one node
-    k_kd_count<<<(int)ntiles, kPartThreads, 0, s>>>(cur[0], cur[1], cur[2], tag.p, n, T, tagg.p);
+    k_kd_count<<<(int)ntiles, kPartThreads, 0, s>>>(Lst, tag.p, n, T, tagg.p);
     PM_HIP_TRY(hipGetLastError());
     k_kd_chunkscan<<<nchunks, kChunk, 0, s>>>(tagg.p, ntiles, tcarry.p, ccarry.p);
     PM_HIP_TRY(hipGetLastError());
     k_kd_chunkcarry<<<1, kChunk, 0, s>>>(ccarry.p, nchunks);
     PM_HIP_TRY(hipGetLastError());
-    k_kd_part<<<(int)ntiles, kPartThreads, 0, s>>>(cur[0], cur[1], cur[2], nxt[0], nxt[1], nxt[2], tag.p, n, T,
-                                                   tcarry.p, ccarry.p);
+    k_kd_part<<<(int)ntiles, kPartThreads, 0, s>>>(Lst, tag.p, n, T, tcarry.p, ccarry.p);
     PM_HIP_TRY(hipGetLastError());
-    for (int d = 0; d < 3; d++) {
-      float4* t = cur[d];
-      cur[d] = nxt[d];
-      nxt[d] = t;
-    }
   }
   return hipSuccess;
 }

@@ -257,6 +257,7 @@ static int wave_lockstep(const float* const* qs, const float* cuts, int policy, 
   return it;
 }
 
+
 static uint32_t part1by2(uint32_t x) {
   x &= 0x3FF;
   x = (x | (x << 16)) & 0x30000FF; x = (x | (x << 8)) & 0x300F00F;
@@ -274,6 +275,52 @@ static double seed_bound(const float* lq, float lt, const float* q) {
   const double c = (sqrt((double)lt) + sqrt(dx * dx + dy * dy + dz * dz)) * (1.0 + 1e-6);
   return c * c * (1.0 + 1e-5) + 1e-30;
 }
+
+// ---- F: wave max steps when the followers of each 256-query block are
+// regrouped into waves by their seeded cut-off (sorted within the block).
+static int cmp_f(const void* a, const void* b) {
+  const float x = *(const float*)a, y = *(const float*)b;
+  return x < y ? -1 : x > y;
+}
+static void regroup_model(const float* Q, const int* ord, long nq, const float* lt, long nl, int blocks) {
+  double morton = 0, sorted = 0, mean = 0;
+  List L;
+  int dummy = 0;
+  srand(777);
+  for (int bk = 0; bk < blocks; bk++) {
+    const long b0 = (long)((double)rand() / RAND_MAX * (nq / 256 - 2)) * 256;
+    float rec[256][2];   // (cut, steps)
+    for (int l = 0; l < 256; l++) {
+      const long r = b0 + l;
+      const float* q = &Q[3 * ord[r]];
+      float cut = nextafterf(R2, 0.f);
+      if (r % STRIDE) {
+        const long jp = r / STRIDE;
+        double b = 1e300;
+        for (long j = jp - 1; j <= jp + 2; j++)
+          if (j >= 0 && j < nl && lt[j] > -2.f) b = fmin(b, seed_bound(&Q[3 * ord[j * STRIDE]], lt[j], q));
+        if (b < cut) cut = (float)b * (1.f + 1e-7f);
+      }
+      rec[l][0] = cut;
+      rec[l][1] = (float)walk_lane(q, cut, &L, &dummy);
+      mean += rec[l][1];
+    }
+    for (int w = 0; w < 4; w++) {
+      float m = 0;
+      for (int l = 0; l < 64; l++) m = fmaxf(m, rec[w * 64 + l][1]);
+      morton += m;
+    }
+    qsort(rec, 256, sizeof(rec[0]), cmp_f);
+    for (int w = 0; w < 4; w++) {
+      float m = 0;
+      for (int l = 0; l < 64; l++) m = fmaxf(m, rec[w * 64 + l][1]);
+      sorted += m;
+    }
+  }
+  printf("F followers regrouped by cut within 256-blocks: mean steps %.1f, wave max Morton %.1f -> sorted %.1f\n",
+         mean / blocks / 256, morton / blocks / 4, sorted / blocks / 4);
+}
+
 
 static float* readf(const char* path, long* n) {
   FILE* f = fopen(path, "rb");
@@ -327,17 +374,20 @@ int main(int argc, char** argv) {
   for (int s = 0; s < sample; s++) waves[s] = (long)((double)rand() / RAND_MAX * (nwaves - 1));
   // only the leaders the sampled waves consult are walked
   char* need = calloc((size_t)nl, 1);
+  const int regroup_blocks = argc > 6 ? atoi(argv[6]) : 0;
   for (int s = 0; s < sample; s++) {
     const long r0 = waves[s] * 64;
     for (long r = r0 - 2 * STRIDE; r < r0 + 64 + 3 * STRIDE; r += STRIDE)
       if (r >= 0 && r / STRIDE < nl) need[r / STRIDE] = 1;
   }
   for (long j = 0; j < nl; j++) {
-    if (!need[j]) continue;
+    lt[j] = -3.f;
+    if (!need[j] && !regroup_blocks) continue;
     walk_lane(&Q[3 * ord[j * STRIDE]], nextafterf(R2, 0.f), &L, &dummy);
     lt[j] = L.n >= K ? key_d2(L.key[K - 1]) : -1.f;
   }
   double a_mean = 0, a_max = 0, a_ins = 0, b_nodes = 0, b_ins = 0, c_nodes = 0, c_buckets = 0, c_pts = 0, c_ins = 0;
+  double e_nodes = 0, e_buckets = 0, e_pts = 0, e_ins = 0, e_max_nodes = 0, e_max_pts = 0, e_max_cost = 0;
   double a_plain_max = 0, b_plain = 0, c_maxins = 0, b_maxins = 0, d_it[2] = {0, 0}, d_rounds[2] = {0, 0}, d_ins[2] = {0, 0};
   for (int s = 0; s < sample; s++) {
     const long r0 = waves[s] * 64;
@@ -375,6 +425,31 @@ int main(int argc, char** argv) {
     a_max += mx;
     a_plain_max += mxp;
     a_ins += ins;
+    // E: per-lane bucketed walk (each lane alone, buckets of <= BUCKET nodes)
+    {
+      double mn = 0, mp = 0, mc = 0;
+      for (int l = 0; l < 64; l++) {
+        Packet* X = malloc(sizeof(Packet));
+        memset(X, 0, sizeof(Packet));
+        X->n = 1;
+        X->q[0] = W.q[l];
+        X->cut[0] = W.cut[l];
+        list_init(&X->L[0]);
+        packet_visit(X, 0, 1);
+        e_nodes += X->nodes;
+        e_buckets += X->buckets;
+        e_pts += X->bucket_pts;
+        e_ins += X->ins;
+        if (X->nodes > mn) mn = X->nodes;
+        if (X->bucket_pts > mp) mp = X->bucket_pts;
+        const double cost = 55.0 * X->nodes + 12.0 * X->bucket_pts;   // VALU model: walk step vs point test
+        if (cost > mc) mc = cost;
+        free(X);
+      }
+      e_max_nodes += mn;
+      e_max_pts += mp;
+      e_max_cost += mc;
+    }
     Wp = W;
     for (int l = 0; l < 64; l++) { list_init(&W.L[l]); Wp.cut[l] = nextafterf(R2, 0.f); list_init(&Wp.L[l]); }
     Wc = W;
@@ -396,6 +471,7 @@ int main(int argc, char** argv) {
     b_maxins += m;
   }
   const double S = sample;
+  if (regroup_blocks) regroup_model(Q, ord, nq, lt, nl, regroup_blocks);
   printf("photons %d queries %ld waves %ld (sampled %d)\n", N, nq, nwaves, sample);
   printf("A per-lane JUMP walk, seeded: loads/lane %.1f, wave max %.1f (plain cut: wave max %.1f), inserts/lane %.1f\n",
          a_mean / S / 64, a_max / S, a_plain_max / S, a_ins / S / 64);
@@ -403,6 +479,10 @@ int main(int argc, char** argv) {
          b_plain / S, b_ins / S / 64, b_maxins / S);
   printf("C packet + %d-node buckets: nodes/wave %.1f, buckets/wave %.1f (%.0f points), inserts/lane %.1f (max lane %.1f)\n",
          BUCKET, c_nodes / S, c_buckets / S, c_pts / S, c_ins / S / 64, c_maxins / S);
+  printf("E per-lane bucketed walk (%d-node buckets): top nodes/lane %.1f (wave max %.1f), buckets/lane %.1f, "
+         "points/lane %.1f (wave max %.1f), inserts/lane %.1f; VALU model wave max %.0f vs A %.0f\n",
+         BUCKET, e_nodes / S / 64, e_max_nodes / S, e_buckets / S / 64, e_pts / S / 64, e_max_pts / S, e_ins / S / 64,
+         e_max_cost / S, 55.0 * a_max / S);
   for (int pol = 0; pol < 2; pol++)
     printf("D lockstep wave (QL %d, %s rounds): iterations %.1f, rounds %.1f, inserts/lane %.1f\n", QL,
            pol ? "batch-merge" : "pop-one", d_it[pol] / S, d_rounds[pol] / S, d_ins[pol] / S / 64);
