@@ -17,8 +17,8 @@
 // buffer holds each of its three lists (SegTab::sel). The lists are SoA (x, y,
 // z, original index as four arrays), so the count pass reads only the split
 // coordinate (and the index on a coordinate tie). Subtree ranges are identical
-// in the three lists, so a single tag array tracks subtree membership. Ties are
-// broken by the original index.
+// in the three lists; a position's subtree is found from the subtree table
+// (k_kd_tileseg + seg_find). Ties are broken by the original index.
 #include <algorithm>
 
 #include "pm_internal.hpp"
@@ -137,13 +137,12 @@ __device__ __forceinline__ int kd_class(const float4 e, int dim, float nc, int n
 //   k_kd_chunkscan / k_kd_chunkcarry  exclusive segmented carry per tile,
 //   k_kd_part      block scan + carry -> stable scatter into the other buffer:
 //                  L -> b + #L before it in the segment, M -> b + ls,
-//                  R -> b + ls + 1 + #R before it; the tag (segment id per
-//                  position) is updated in place.
+//                  R -> b + ls + 1 + #R before it.
 // Kernel boundaries order the passes (a decoupled look-back needs agent-scope
 // release fences per tile, i.e. L2 write-backs across the 8 XCDs: measured
-// 7 ms per level). Traffic per element and level: count 2 x 4 B + tag, part
-// 2 x 16 B read + 2 x 16 B written + tag read / write (84 B; the AoS lists that
-// moved all three 16-B lists took 140 B).
+// 7 ms per level). Traffic per element and level: count 2 x 4 B, part 2 x 16 B
+// read + 2 x 16 B written (72 B; the AoS lists that moved all three 16-B lists
+// and a segment tag per position took 140 B).
 // Occupancy targets (waves per SIMD, 0 = compiler's choice), build-time A/B knobs.
 #ifndef PM_KD_PART_WAVES
 #define PM_KD_PART_WAVES 0
@@ -214,40 +213,117 @@ __device__ __forceinline__ SegVal block_seg_scan(const SegVal& th, SegVal* sh, S
   return seg_combine(wpre, ex);
 }
 
+// Segment lookup without a per-position tag array: the segments of a level are
+// the heap nodes t = 2^L - 1 + j, j = 0 .. 2^L - 1, left to right with
+// non-decreasing starts b_j (a gap between two holds the medians of earlier
+// levels: placed positions). k_kd_tileseg finds, per 512-position tile, the
+// last segment starting at or before the tile; a block then knows that its
+// positions lie in segments jl .. jh (jh: the next tile's first). Up to
+// kSegCache records are staged in LDS (the usual case: a global-level segment
+// holds >= 1023 positions, so a tile meets one or two); more (the check
+// variant's tiny deep segments) fall back to a binary search in global memory.
+// This replaced a 4-B tag per position read by both passes and rewritten by
+// the part pass, and the per-position dependent loads of the segment record.
+constexpr int kSegCache = 8;
+
+struct SegRec {
+  int b, s, ls, dim, id, sel;
+  float coord;
+};
+
+__device__ __forceinline__ SegRec seg_load(const SegTab& T, int64_t t) {
+  SegRec r;
+  r.b = T.b[t];
+  r.s = T.s[t];
+  r.ls = T.ls[t];
+  r.dim = T.dim[t];
+  r.id = T.id[t];
+  r.sel = T.sel[t];
+  r.coord = T.coord[t];
+  return r;
+}
+
+__global__ void k_kd_tileseg(const int32_t* __restrict__ tb, int level, int64_t ntiles, int32_t* __restrict__ tile_seg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > ntiles) return;
+  const int64_t base = (1ll << level) - 1, nseg = 1ll << level;
+  const int64_t p = i < ntiles ? i * kPartTile : INT64_MAX;
+  int64_t lo = 0, hi = nseg;   // last j with b_j <= p (b_0 = 0)
+  while (hi - lo > 1) {
+    const int64_t m = (lo + hi) >> 1;
+    if ((int64_t)tb[base + m] <= p) lo = m;
+    else hi = m;
+  }
+  tile_seg[i] = (int32_t)lo;
+}
+
+// Per-block view of the segments [jl, jh] that can hold the block's positions.
+struct TileSegs {
+  int jl, jh;
+  bool cached;
+};
+
+__device__ __forceinline__ TileSegs tile_segs(const SegTab& T, int level, const int32_t* __restrict__ tile_seg,
+                                              SegRec* cache) {
+  TileSegs ts;
+  ts.jl = tile_seg[blockIdx.x];
+  ts.jh = tile_seg[blockIdx.x + 1];
+  ts.cached = ts.jh - ts.jl < kSegCache;
+  const int64_t base = (1ll << level) - 1;
+  if (ts.cached && (int)threadIdx.x <= ts.jh - ts.jl) cache[threadIdx.x] = seg_load(T, base + ts.jl + threadIdx.x);
+  __syncthreads();
+  return ts;
+}
+
+// segment of position p (false: p is a placed median / outside every segment)
+__device__ __forceinline__ bool seg_find(const SegTab& T, int level, const TileSegs& ts, const SegRec* cache,
+                                         int64_t p, SegRec& r) {
+  if (ts.cached) {
+    int k = 0;
+    for (int c = 1; c <= ts.jh - ts.jl; c++)
+      if ((int64_t)cache[c].b <= p) k = c;
+    r = cache[k];
+  } else {
+    const int64_t base = (1ll << level) - 1;
+    int lo = ts.jl, hi = ts.jh + 1;
+    while (hi - lo > 1) {
+      const int m = (lo + hi) >> 1;
+      if ((int64_t)T.b[base + m] <= p) lo = m;
+      else hi = m;
+    }
+    r = seg_load(T, base + lo);
+  }
+  return r.s > 0 && p >= r.b && p < (int64_t)r.b + r.s;
+}
+
 // Striped tiles: item k of thread i sits at position tile*512 + k*256 + i, so
 // every wave access covers 64 consecutive positions; the segmented scan runs
 // once per k-round, carried across rounds.
 struct PartItem {
-  int tg, sb, sls, sel;
+  int sb, sls, sel;
+  bool live;
   uint8_t cls[3];   // 0 L, 1 M, 2 R, 3 not moved (split list / placed / out of range)
 };
 
 // Classes of position p in the three lists; KEEP: also load the moved
 // elements (into e[d]). The split list is never loaded (positional).
 template <bool KEEP>
-__device__ __forceinline__ SegVal part_load(const KdLists& Lst, const int32_t* __restrict__ tag, int64_t n,
-                                            const SegTab& T, int64_t p, PartItem& it, float4 (&e)[3]) {
+__device__ __forceinline__ SegVal part_load(const KdLists& Lst, int64_t n, const SegTab& T, int level,
+                                            const TileSegs& ts, const SegRec* cache, int64_t p, PartItem& it,
+                                            float4 (&e)[3]) {
   SegVal th = seg_zero();
-  it.tg = p < n ? tag[p] : -1;
-  int dim = 0, nid = 0;
-  float nc = 0.f;
-  it.sb = 0;
-  it.sls = 0;
-  it.sel = 0;
-  if (it.tg >= 0) {
-    const int t = it.tg;
-    it.sb = T.b[t];
-    it.sls = T.ls[t];
-    it.sel = T.sel[t];
-    dim = T.dim[t];
-    nc = T.coord[t];
-    nid = T.id[t];
-  }
-  th.f = it.tg >= 0 && p == it.sb;
+  SegRec r{};
+  it.live = p < n && seg_find(T, level, ts, cache, p, r);
+  it.sb = r.b;
+  it.sls = r.ls;
+  it.sel = r.sel;
+  const int dim = r.dim, nid = r.id;
+  const float nc = r.coord;
+  th.f = it.live && p == it.sb;
 #pragma unroll
   for (int d = 0; d < 3; d++) {
     int c = 3;
-    if (it.tg >= 0 && d != dim) {
+    if (it.live && d != dim) {
       const int k = (it.sel >> d) & 1;
       if (KEEP) {
         e[d] = kd_elem(Lst, d, k, p);
@@ -270,17 +346,20 @@ __device__ __forceinline__ SegVal part_load(const KdLists& Lst, const int32_t* _
   return th;
 }
 
-__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void k_kd_count(KdLists Lst,
-                                                           const int32_t* __restrict__ tag, int64_t n, SegTab T,
+__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void k_kd_count(KdLists Lst, int64_t n,
+                                                           SegTab T, int level,
+                                                           const int32_t* __restrict__ tile_seg,
                                                            SegVal* __restrict__ tile_agg) {
   __shared__ SegVal sh[kPartThreads / 64];
+  __shared__ SegRec cache[kSegCache];
+  const TileSegs ts = tile_segs(T, level, tile_seg, cache);
   const int64_t base = (int64_t)blockIdx.x * kPartTile + threadIdx.x;
   SegVal th[kPartIPT];
   float4 dummy[3];
 #pragma unroll
   for (int k = 0; k < kPartIPT; k++) {
     PartItem it;
-    th[k] = part_load<false>(Lst, tag, n, T, base + k * kPartThreads, it, dummy);
+    th[k] = part_load<false>(Lst, n, T, level, ts, cache, base + k * kPartThreads, it, dummy);
   }
   SegVal agg = seg_zero();
 #pragma unroll
@@ -322,17 +401,21 @@ __global__ __launch_bounds__(kChunk) void k_kd_chunkcarry(SegVal* __restrict__ c
   }
 }
 
-__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void k_kd_part(KdLists Lst,
-                                                          int32_t* __restrict__ tag, int64_t n, SegTab T,
+__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void k_kd_part(KdLists Lst, int64_t n,
+                                                          SegTab T, int level,
+                                                          const int32_t* __restrict__ tile_seg,
                                                           const SegVal* __restrict__ tile_carry,
                                                           const SegVal* __restrict__ chunk_carry) {
   __shared__ SegVal sh[kPartThreads / 64];
+  __shared__ SegRec cache[kSegCache];
+  const TileSegs ts = tile_segs(T, level, tile_seg, cache);
   const int64_t base = (int64_t)blockIdx.x * kPartTile + threadIdx.x;
   PartItem it[kPartIPT];
   float4 e[kPartIPT][3];
   SegVal th[kPartIPT];
 #pragma unroll
-  for (int k = 0; k < kPartIPT; k++) th[k] = part_load<true>(Lst, tag, n, T, base + k * kPartThreads, it[k], e[k]);
+  for (int k = 0; k < kPartIPT; k++)
+    th[k] = part_load<true>(Lst, n, T, level, ts, cache, base + k * kPartThreads, it[k], e[k]);
   SegVal carry = seg_combine(chunk_carry[blockIdx.x / kChunk], tile_carry[blockIdx.x]);
 #pragma unroll
   for (int k = 0; k < kPartIPT; k++) {
@@ -356,11 +439,6 @@ __global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void 
       Lst.comp(d, ko, 1)[dst] = e[k][d].y;
       Lst.comp(d, ko, 2)[dst] = e[k][d].z;
       Lst.comp(d, ko, 3)[dst] = e[k][d].w;
-    }
-    if (it[k].tg >= 0) {
-      const int t = it[k].tg;
-      const int64_t mid = it[k].sb + it[k].sls;
-      tag[p] = p < mid ? 2 * t + 1 : (p == mid ? -1 : 2 * t + 2);
     }
   }
 }
@@ -584,20 +662,20 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
       PM_HIP_TRY(hipGetLastError());
     }
   }
-  DevBuf<int32_t> tb(cap), ts(cap), tls(cap), tdim(cap), tid(cap), tsel(cap), tag(n);
+  DevBuf<int32_t> tb(cap), ts(cap), tls(cap), tdim(cap), tid(cap), tsel(cap);
   DevBuf<float> tco(cap);
   const int64_t ntiles = (n + kPartTile - 1) / kPartTile;
   const int nchunks = (int)((ntiles + kChunk - 1) / kChunk);
   DevBuf<SegVal> tagg(ntiles), tcarry(ntiles), ccarry(nchunks);
-  if (!tb.p || !ts.p || !tls.p || !tdim.p || !tid.p || !tsel.p || !tag.p || !tco.p || !tagg.p || !tcarry.p ||
-      !ccarry.p)
+  DevBuf<int32_t> tile_seg(ntiles + 1);
+  if (!tb.p || !ts.p || !tls.p || !tdim.p || !tid.p || !tsel.p || !tco.p || !tagg.p || !tcarry.p || !ccarry.p ||
+      !tile_seg.p)
     return hipErrorOutOfMemory;
   SegTab T{tb.p, ts.p, tls.p, tdim.p, tco.p, tid.p, tsel.p};
   const int32_t root[3] = {0, (int32_t)n, 0};
   PM_HIP_TRY(hipMemcpyAsync(tb.p, &root[0], 4, hipMemcpyHostToDevice, s));
   PM_HIP_TRY(hipMemcpyAsync(ts.p, &root[1], 4, hipMemcpyHostToDevice, s));
   PM_HIP_TRY(hipMemcpyAsync(tsel.p, &root[2], 4, hipMemcpyHostToDevice, s));
-  PM_HIP_TRY(hipMemsetAsync(tag.p, 0, sizeof(int32_t) * n, s));
   // segments at L0 hold <= 1023 elements; the check variant keeps every level
   // global (the identical-tree test compares the two libraries)
   const int L0 = PM_CHECK_VARIANT ? H : std::max(0, H - 10);
@@ -611,13 +689,15 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
     k_kd_seg<<<grid_for(nseg, 256), 256, 0, s>>>(Lst, L, cap, T, nodes);
     PM_HIP_TRY(hipGetLastError());
     if (L == H - 1) break;   // last level: every remaining subtree has one node
-    k_kd_count<<<(int)ntiles, kPartThreads, 0, s>>>(Lst, tag.p, n, T, tagg.p);
+    k_kd_tileseg<<<grid_for(ntiles + 1, 256), 256, 0, s>>>(tb.p, L, ntiles, tile_seg.p);
+    PM_HIP_TRY(hipGetLastError());
+    k_kd_count<<<(int)ntiles, kPartThreads, 0, s>>>(Lst, n, T, L, tile_seg.p, tagg.p);
     PM_HIP_TRY(hipGetLastError());
     k_kd_chunkscan<<<nchunks, kChunk, 0, s>>>(tagg.p, ntiles, tcarry.p, ccarry.p);
     PM_HIP_TRY(hipGetLastError());
     k_kd_chunkcarry<<<1, kChunk, 0, s>>>(ccarry.p, nchunks);
     PM_HIP_TRY(hipGetLastError());
-    k_kd_part<<<(int)ntiles, kPartThreads, 0, s>>>(Lst, tag.p, n, T, tcarry.p, ccarry.p);
+    k_kd_part<<<(int)ntiles, kPartThreads, 0, s>>>(Lst, n, T, L, tile_seg.p, tcarry.p, ccarry.p);
     PM_HIP_TRY(hipGetLastError());
   }
   return hipSuccess;
