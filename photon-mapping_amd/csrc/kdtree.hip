@@ -133,9 +133,11 @@ __device__ __forceinline__ int kd_class(const float4 e, int dim, float nc, int n
 // (L / M / R; the split list and placed positions: 3) and the packed (L, R)
 // counts are scanned SEGMENTED (reset at segment starts):
 //   k_kd_count     per-tile segmented aggregate (reads the split coordinate,
-//                  the index only on a coordinate tie),
+//                  the index only on a coordinate tie; a block sum of packed
+//                  tile-local counts),
 //   k_kd_chunkscan / k_kd_chunkcarry  exclusive segmented carry per tile,
-//   k_kd_part      block scan + carry -> stable scatter into the other buffer:
+//   k_kd_part      block scan of the packed counts + carry -> stable scatter
+//                  into the other buffer:
 //                  L -> b + #L before it in the segment, M -> b + ls,
 //                  R -> b + ls + 1 + #R before it.
 // Kernel boundaries order the passes (a decoupled look-back needs agent-scope
@@ -261,6 +263,7 @@ __global__ void k_kd_tileseg(const int32_t* __restrict__ tb, int level, int64_t 
 struct TileSegs {
   int jl, jh;
   bool cached;
+  int64_t last_start;   // largest start of a (non-empty) subtree inside the tile, -1: none
 };
 
 __device__ __forceinline__ TileSegs tile_segs(const SegTab& T, int level, const int32_t* __restrict__ tile_seg,
@@ -270,8 +273,17 @@ __device__ __forceinline__ TileSegs tile_segs(const SegTab& T, int level, const 
   ts.jh = tile_seg[blockIdx.x + 1];
   ts.cached = ts.jh - ts.jl < kSegCache;
   const int64_t base = (1ll << level) - 1;
-  if (ts.cached && (int)threadIdx.x <= ts.jh - ts.jl) cache[threadIdx.x] = seg_load(T, base + ts.jl + threadIdx.x);
+  const int64_t t0 = (int64_t)blockIdx.x * kPartTile;
+  __shared__ long long s_last;
+  if (threadIdx.x == 0) s_last = -1;
   __syncthreads();
+  for (int j = ts.jl + (int)threadIdx.x; j <= ts.jh; j += blockDim.x) {
+    const SegRec r = seg_load(T, base + j);
+    if (ts.cached) cache[j - ts.jl] = r;
+    if (r.s > 0 && r.b >= t0 && r.b < t0 + kPartTile) atomicMax(&s_last, (long long)r.b);
+  }
+  __syncthreads();
+  ts.last_start = s_last;
   return ts;
 }
 
@@ -346,29 +358,58 @@ __device__ __forceinline__ SegVal part_load(const KdLists& Lst, int64_t n, const
   return th;
 }
 
+// Tile-local counts packed in one u64: list d's L count at bits 20d, its R
+// count at bits 20d + 10 (a tile has 512 positions: 10 bits per field).
+__device__ __forceinline__ uint64_t pack_cls(const PartItem& it) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int d = 0; d < 3; d++)
+    v |= (uint64_t)(it.cls[d] == 0) << (20 * d) | (uint64_t)(it.cls[d] == 2) << (20 * d + 10);
+  return v;
+}
+__device__ __forceinline__ uint32_t field_l(uint64_t v, int d) { return (uint32_t)(v >> (20 * d)) & 1023u; }
+__device__ __forceinline__ uint32_t field_r(uint64_t v, int d) { return (uint32_t)(v >> (20 * d + 10)) & 1023u; }
+
+// Block-wide sum of a u64 (blockDim = kPartThreads).
+__device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, uint64_t* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = 0;
+#pragma unroll
+  for (int w = 0; w < kPartThreads / 64; w++) t += sh[w];
+  return t;
+}
+
+// Per-tile segmented aggregate: the (L, R) counts of the positions at or after
+// the last subtree start inside the tile (all positions if none starts in it),
+// and whether one starts -- a plain block sum, no scan.
 __global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void k_kd_count(KdLists Lst, int64_t n,
                                                            SegTab T, int level,
                                                            const int32_t* __restrict__ tile_seg,
                                                            SegVal* __restrict__ tile_agg) {
-  __shared__ SegVal sh[kPartThreads / 64];
   __shared__ SegRec cache[kSegCache];
+  __shared__ uint64_t sh[kPartThreads / 64];
   const TileSegs ts = tile_segs(T, level, tile_seg, cache);
   const int64_t base = (int64_t)blockIdx.x * kPartTile + threadIdx.x;
-  SegVal th[kPartIPT];
+  uint64_t sum = 0;
   float4 dummy[3];
 #pragma unroll
   for (int k = 0; k < kPartIPT; k++) {
     PartItem it;
-    th[k] = part_load<false>(Lst, n, T, level, ts, cache, base + k * kPartThreads, it, dummy);
+    const int64_t p = base + k * kPartThreads;
+    part_load<false>(Lst, n, T, level, ts, cache, p, it, dummy);
+    if (p >= ts.last_start) sum += pack_cls(it);
   }
-  SegVal agg = seg_zero();
+  sum = block_sum_u64(sum, sh);
+  if (threadIdx.x == 0) {
+    SegVal agg;
 #pragma unroll
-  for (int k = 0; k < kPartIPT; k++) {
-    SegVal total;
-    block_seg_scan<kPartThreads / 64>(th[k], sh, total);
-    agg = seg_combine(agg, total);
+    for (int d = 0; d < 3; d++) agg.v[d] = (uint64_t)field_l(sum, d) | (uint64_t)field_r(sum, d) << 32;
+    agg.f = ts.last_start >= 0;
+    tile_agg[blockIdx.x] = agg;
   }
-  if (threadIdx.x == 0) tile_agg[blockIdx.x] = agg;
 }
 
 // Exclusive segmented prefix over the tile aggregates in two coalesced steps:
@@ -401,39 +442,76 @@ __global__ __launch_bounds__(kChunk) void k_kd_chunkcarry(SegVal* __restrict__ c
   }
 }
 
+// Block-wide inclusive scan of a u64 (blockDim = kPartThreads); total out.
+__device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sh, uint64_t& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t up = __shfl_up(v, o);
+    if (lane >= o) v += up;
+  }
+  if (lane == 63) sh[wave] = v;
+  __syncthreads();
+  uint64_t pre = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < kPartThreads / 64; w++) {
+    if (w < wave) pre += sh[w];
+    total += sh[w];
+  }
+  __syncthreads();   // sh is reused by the next call
+  return pre + v;
+}
+
+// Stable scatter of the tile's moving elements: a plain exclusive scan of the
+// packed tile-local counts gives each position the counts before it in the
+// tile; a subtree that starts inside the tile subtracts the prefix at its
+// start, one that started before adds the carry of the earlier tiles.
 __global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void k_kd_part(KdLists Lst, int64_t n,
                                                           SegTab T, int level,
                                                           const int32_t* __restrict__ tile_seg,
                                                           const SegVal* __restrict__ tile_carry,
                                                           const SegVal* __restrict__ chunk_carry) {
-  __shared__ SegVal sh[kPartThreads / 64];
   __shared__ SegRec cache[kSegCache];
+  __shared__ uint64_t sh[kPartThreads / 64];
+  __shared__ uint64_t pre[kPartTile];   // exclusive tile-local prefix per position
   const TileSegs ts = tile_segs(T, level, tile_seg, cache);
-  const int64_t base = (int64_t)blockIdx.x * kPartTile + threadIdx.x;
+  const int64_t t0 = (int64_t)blockIdx.x * kPartTile;
+  const int64_t base = t0 + threadIdx.x;
   PartItem it[kPartIPT];
   float4 e[kPartIPT][3];
-  SegVal th[kPartIPT];
-#pragma unroll
-  for (int k = 0; k < kPartIPT; k++)
-    th[k] = part_load<true>(Lst, n, T, level, ts, cache, base + k * kPartThreads, it[k], e[k]);
-  SegVal carry = seg_combine(chunk_carry[blockIdx.x / kChunk], tile_carry[blockIdx.x]);
+  uint64_t run = 0;
 #pragma unroll
   for (int k = 0; k < kPartIPT; k++) {
-    SegVal total;
-    const SegVal ex = block_seg_scan<kPartThreads / 64>(th[k], sh, total);
-    SegVal run = seg_combine(carry, ex);   // counts before this position in its segment
-    carry = seg_combine(carry, total);
+    part_load<true>(Lst, n, T, level, ts, cache, base + k * kPartThreads, it[k], e[k]);
+    const uint64_t v = pack_cls(it[k]);
+    uint64_t total;
+    const uint64_t inc = block_scan_u64(v, sh, total);
+    pre[k * kPartThreads + threadIdx.x] = run + inc - v;
+    run += total;
+  }
+  __syncthreads();
+  const SegVal carry = seg_combine(chunk_carry[blockIdx.x / kChunk], tile_carry[blockIdx.x]);
+#pragma unroll
+  for (int k = 0; k < kPartIPT; k++) {
     const int64_t p = base + k * kPartThreads;
-    if (p >= n) continue;
-    if (th[k].f) run = seg_zero();
+    if (!it[k].live) continue;
+    const uint64_t mine = pre[p - t0];
+    const bool inside = it[k].sb >= t0;   // the subtree starts in this tile
+    const uint64_t before = inside ? mine - pre[it[k].sb - t0] : mine;   // field-wise (prefixes only grow)
 #pragma unroll
     for (int d = 0; d < 3; d++) {
       const int c = it[k].cls[d];
       if (c == 3) continue;
       int64_t dst;
-      if (c == 0) dst = it[k].sb + (int64_t)(uint32_t)run.v[d];
-      else if (c == 1) dst = it[k].sb + it[k].sls;
-      else dst = it[k].sb + it[k].sls + 1 + (int64_t)(uint32_t)(run.v[d] >> 32);
+      if (c == 0) {
+        dst = it[k].sb + (int64_t)field_l(before, d) + (inside ? 0 : (int64_t)(uint32_t)carry.v[d]);
+      } else if (c == 1) {
+        dst = it[k].sb + it[k].sls;
+      } else {
+        dst = it[k].sb + it[k].sls + 1 + (int64_t)field_r(before, d) +
+              (inside ? 0 : (int64_t)(uint32_t)(carry.v[d] >> 32));
+      }
       const int ko = ((it[k].sel >> d) & 1) ^ 1;
       Lst.comp(d, ko, 0)[dst] = e[k][d].x;
       Lst.comp(d, ko, 1)[dst] = e[k][d].y;
