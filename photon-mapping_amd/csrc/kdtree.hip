@@ -442,7 +442,11 @@ __global__ __launch_bounds__(kChunk) void k_kd_chunkcarry(SegVal* __restrict__ c
   }
 }
 
-// Block-wide inclusive scan of a u64 (blockDim = kPartThreads); total out.
+// Block-wide inclusive scan of a u64 (blockDim = W * 64, W <= 64); total out.
+// `sh` holds W + 1 entries: wave totals, then (after wave 0 scanned them) the
+// exclusive wave prefixes and the block total, so a thread reads two values
+// whatever W is (a per-thread loop over W loads kept 2W VGPRs live).
+template <int W = kPartThreads / 64>
 __device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sh, uint64_t& total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -452,13 +456,20 @@ __device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t* sh, uin
   }
   if (lane == 63) sh[wave] = v;
   __syncthreads();
-  uint64_t pre = 0;
-  total = 0;
+  if (wave == 0) {
+    uint64_t x = lane < W ? sh[lane] : 0ull;
 #pragma unroll
-  for (int w = 0; w < kPartThreads / 64; w++) {
-    if (w < wave) pre += sh[w];
-    total += sh[w];
+    for (int o = 1; o < W; o <<= 1) {
+      const uint64_t up = __shfl_up(x, o);
+      if (lane >= o) x += up;
+    }
+    if (lane == W - 1) sh[W] = x;
+    const uint64_t ex = __shfl_up(x, 1);
+    if (lane < W) sh[lane] = lane == 0 ? 0ull : ex;
   }
+  __syncthreads();
+  const uint64_t pre = sh[wave];
+  total = sh[W];
   __syncthreads();   // sh is reused by the next call
   return pre + v;
 }
@@ -473,7 +484,7 @@ __global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void 
                                                           const SegVal* __restrict__ tile_carry,
                                                           const SegVal* __restrict__ chunk_carry) {
   __shared__ SegRec cache[kSegCache];
-  __shared__ uint64_t sh[kPartThreads / 64];
+  __shared__ uint64_t sh[kPartThreads / 64 + 1];
   __shared__ uint64_t pre[kPartTile];   // exclusive tile-local prefix per position
   const TileSegs ts = tile_segs(T, level, tile_seg, cache);
   const int64_t t0 = (int64_t)blockIdx.x * kPartTile;
@@ -547,7 +558,8 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
   __shared__ uint8_t sdim[kLocal / 2];
   __shared__ float sco[kLocal / 2];
   __shared__ int32_t sid[kLocal / 2];
-  __shared__ SegVal sh[kLocal / 64];
+  __shared__ uint64_t sh[kLocal / 64 + 1];
+  __shared__ uint64_t spre[1 << kLocalWaveLevel];   // packed-count prefix at each sub-segment's start
   __shared__ float4 stage[kLocal];   // this subtree's nodes by local heap index (w = -1: none)
   const int tid = threadIdx.x;
   const int64_t t = ((int64_t)1 << L0) - 1 + blockIdx.x;
@@ -600,33 +612,37 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     }
     if (k + 1 == H) break;
     __syncthreads();
-    // class, segmented scan and in-place stable scatter of the three lists
+    // class, scan of the packed counts (10 bits per field: a sub-segment holds
+    // <= 1023) and in-place stable scatter of the three lists; counts before a
+    // position in its sub-segment = its exclusive prefix - the prefix at the
+    // sub-segment's start (block levels: <= 8 sub-segments)
     const int j = tag[tid];
     float4 e[3];
     uint8_t c[3];
-    SegVal th = seg_zero();
+    uint64_t v = 0;
     int b = 0, ls = 0;
     if (j >= 0) {
       b = sb[cur][j];
       ls = sls[j];
-      th.f = tid == b;
     }
 #pragma unroll
     for (int d = 0; d < 3; d++) {
       e[d] = buf[d][tid];
       c[d] = j < 0 ? 3 : (uint8_t)kd_class(e[d], sdim[j >= 0 ? j : 0], sco[j >= 0 ? j : 0], sid[j >= 0 ? j : 0]);
-      th.v[d] = c[d] == 0 ? 1ull : (c[d] == 2 ? (1ull << 32) : 0ull);
+      v |= (uint64_t)(c[d] == 0) << (20 * d) | (uint64_t)(c[d] == 2) << (20 * d + 10);
     }
-    SegVal total;
-    SegVal ex = block_seg_scan<kLocal / 64>(th, sh, total);   // ends with a barrier: all reads done
-    if (th.f) ex = seg_zero();
+    uint64_t total;
+    const uint64_t inc = block_scan_u64<kLocal / 64>(v, sh, total);   // ends with a barrier: all reads done
+    if (j >= 0 && tid == b) spre[j] = inc - v;
+    __syncthreads();
+    const uint64_t before = inc - v - (j >= 0 ? spre[j] : 0ull);
 #pragma unroll
     for (int d = 0; d < 3; d++) {
       int dst;
       if (c[d] == 3) dst = tid;
-      else if (c[d] == 0) dst = b + (int)(uint32_t)ex.v[d];
+      else if (c[d] == 0) dst = b + (int)field_l(before, d);
       else if (c[d] == 1) dst = b + ls;
-      else dst = b + ls + 1 + (int)(uint32_t)(ex.v[d] >> 32);
+      else dst = b + ls + 1 + (int)field_r(before, d);
       if (tid < S) buf[d][dst] = e[d];
     }
     if (j >= 0) tag[tid] = (int16_t)(tid < b + ls ? 2 * j : (tid == b + ls ? -1 : 2 * j + 1));
