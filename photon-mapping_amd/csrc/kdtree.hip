@@ -160,6 +160,7 @@ constexpr int kPartThreads = 256;
 #endif
 constexpr int kPartIPT = PM_KD_IPT;
 constexpr int kPartTile = kPartThreads * kPartIPT;   // positions per tile
+static_assert(kPartTile < 1024, "tile-local counts are packed in 10-bit fields (pack_cls)");
 
 struct SegVal {   // segmented-scan value: packed (L | R << 32) count per list
   uint64_t v[3];
