@@ -256,8 +256,8 @@ def main():
         "photon_maps": {"global": info["n_global"], "caustic": info["n_caustic"]},
         "render": {"path_vertices": int(st.path_vertices), "caustic_queries": int(st.caustic_queries),
                    "global_queries": nq_g, "rays": int(st.rays)},
-        "roofline": {"bound": "hbm", "kernel": ("pmd::k_gather_level<1, 8, true> (global-map kNN radiance estimate: one phase, one launch "
-                                "per seed level; time = all of them, HIP events on the launch stream)"),
+        "roofline": {"bound": "hbm", "kernel": ("pmd::k_gather_level<1, LEADERS> (global-map kNN radiance estimate: one phase, a "
+                                "leader launch + a follower launch; time = both, HIP events on the launch stream)"),
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "bytes_per_query": bpq, "queries_per_launch": nq_g,
