@@ -67,7 +67,7 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
     counts_g = oracle.photons_per_light(lights, args.casted)
     counts_c = oracle.photons_per_light(lights, args.caustic)
     P = sum(counts_g) + sum(counts_c)
-    frac = args.cpu_sample_photons / max(1, sum(counts_g))
+    frac = min(1.0, args.cpu_sample_photons / max(1, sum(counts_g)))
     sg = int(sum(counts_g) * frac)
     scn = int(sum(counts_c) * frac)
     t = time.time()
@@ -107,24 +107,36 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=3, choices=[3, 5],
-                    help="3: Sponza-class, 10M + 1M photons per GPU (the headline line); 5: caustics pass, "
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5],
+                    help="3: Sponza-class, 10M + 1M photons per GPU (the headline line); 2: Cornell box "
+                         "(the reference's cornell-box.glb), 1M + 1M photons, 512x512; 5: caustics pass, "
                          "square area light + glass, 6.25M caustic photons per GPU (50M at 8), k = 200")
-    ap.add_argument("--casted", type=int, default=10_000_000, help="diffuse photons per GPU")
-    ap.add_argument("--caustic", type=int, default=None, help="caustic photons per GPU (config 3: 1M, 5: 6.25M)")
+    ap.add_argument("--casted", type=int, default=None, help="diffuse photons per GPU (config 2: 1M, 3/5: 10M)")
+    ap.add_argument("--caustic", type=int, default=None,
+                    help="caustic photons per GPU (config 2: 1M, 3: 1M, 5: 6.25M)")
     ap.add_argument("--caustic-k", type=int, default=None, help="caustic gather neighbours (config 3: 50, 5: 200)")
     ap.add_argument("--max-depth", type=int, default=10)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=None, help="config 2: 512, 3/5: 1920")
+    ap.add_argument("--height", type=int, default=None, help="config 2: 512, 3/5: 1080")
     ap.add_argument("--spp", type=int, default=1)
     ap.add_argument("--depth", type=int, default=30)
-    ap.add_argument("--scene", default="sponza", choices=["sponza", "cornell"])
+    ap.add_argument("--scene", default=None, choices=["sponza", "cornell"],
+                    help="config 2: cornell, 3/5: sponza")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: every CPU this process may use, see host_cores)")
     ap.add_argument("--cpu-sample-photons", type=int, default=2_000_000)
     ap.add_argument("--cpu-sample-rows", type=int, default=48)
     args = ap.parse_args()
+    c2 = args.config == 2
+    if args.scene is None:
+        args.scene = "cornell" if c2 else "sponza"
+    if args.casted is None:
+        args.casted = 1_000_000 if c2 else 10_000_000
+    if args.width is None:
+        args.width = 512 if c2 else 1920
+    if args.height is None:
+        args.height = 512 if c2 else 1080
     if args.caustic is None:
         args.caustic = 6_250_000 if args.config == 5 else 1_000_000
     if args.caustic_k is None:
