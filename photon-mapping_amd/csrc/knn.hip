@@ -170,119 +170,121 @@ __device__ __forceinline__ float lean_cut(float r2) { return __uint_as_float(__f
 //    close-child ancestor-or-self (one step, one cached load), where the
 //    post-order point test and the far decision run. Same visited set, same
 //    point tests, fewer dependent loads.
-// Walk state of one lane (knn_walk_lean).
+//  - The kernel is VALU-issue bound (round 2: ~62 VALU per step x ~460 steps
+//    plus ~111 per insert round x ~165 rounds per wave account for the whole
+//    follower launch at 2.4 GHz), so the step is written for instruction
+//    count: a lane arrives at a node either from its parent or from its close
+//    child (JUMP never returns from a far child), so one `up` flag replaces
+//    the previous-node index; the three transitions are computed branch-free
+//    and selected; the node offset is 32-bit (saddr loads) when the map fits.
+// Gather keys: (d^2 bits << 32 | node word), the node word being the kd node's
+// (orig << 2 | dim) -- orig is unique, so the order is (d^2, orig) as for
+// key_make -- held as a double WITHOUT the 2^52 bias: every key is a
+// non-negative double (zero, denormal or normal; never -0, inf or NaN), whose
+// IEEE order is the integer order because the kernels keep f64 denormals
+// (float_denorm_mode_16_64 = 3). No instruction builds a key.
+__device__ __forceinline__ double gkey(float d2, uint32_t word) {
+  return __longlong_as_double((long long)(((uint64_t)__float_as_uint(d2) << 32) | word));
+}
+__device__ __forceinline__ float gkey_d2(double k) { return __uint_as_float((uint32_t)((uint64_t)__double_as_longlong(k) >> 32)); }
+__device__ __forceinline__ uint32_t gkey_word(double k) { return (uint32_t)__double_as_longlong(k); }
+constexpr uint32_t kNoWord = 0xFFFFFFFFu;   // sentinel's low word (never a node word: orig < 2^29)
+
+// Walk state of one lane (knn_walk_lean). Nodes are numbered from 1 here (c1 =
+// implicit index + 1: children 2 c1, 2 c1 + 1, parent c1 >> 1).
 struct LeanWalk {
   float bound;
-  int prev, curr;
-  uint32_t far_mask;   // JUMP: bit d set <=> the path's depth-d node is a far child
-  int depth;           // JUMP: depth of curr
+  uint32_t c1;
+  uint32_t far_mask;   // bit j set <=> ancestor-or-self c1 >> j was entered as its parent's FAR child
+  bool up;             // arrived at c1 from its close child: its point test is due
   bool walking;
-  int qn;              // queued candidates in this lane's LDS column
+  int qn;              // queued candidates in this lane's LDS column (slots 1..QL; slot 0 = DBL_MAX)
   __device__ __forceinline__ void start(float b, bool valid) {
     bound = b;
-    prev = -1;
-    curr = 0;
-    far_mask = 0;
-    depth = 0;
+    c1 = 1;
+    far_mask = 0;   // the root's bit stays 0: a jump that reaches it ends the walk
+    up = false;
     walking = valid;
   }
 };
 
+// node c1 (1-based): a 32-bit byte offset (saddr load, -16 folded into the
+// instruction) while the map has < 2^28 nodes, 64-bit addressing above
+template <bool WIDE>
+__device__ __forceinline__ float4 node1(const float4* __restrict__ nodes, uint32_t c1) {
+  if (WIDE) return nodes[(size_t)c1 - 1];
+  return *(const float4*)((const char*)nodes - 16 + (c1 << 4));
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 // One walk step of every lane (finished / idle lanes re-read their last node and
 // are masked): the post-order point test queues a candidate, the walk moves on.
-template <int K, bool JUMP>
-__device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, int n, v3 q, const double (&list)[K],
+// Transitions (all computed, one selected):
+//  - descend to the close child (arrived from the parent and it exists);
+//  - else enter the far child if it exists and the plane is within the bound;
+//  - else JUMP: a = c1 >> j with j the lowest clear bit of far_mask is the
+//    deepest close-child ancestor-or-self; go to its parent c1 >> (j + 1)
+//    (arriving from the close child a), or stop when a is the root.
+template <int K, bool WIDE>
+__device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, uint32_t n, v3 q, double tail,
                                           LeanWalk& w, double* lq, int lstride) {
-  const float4 nd = nodes[w.curr];
-  const int child = 2 * w.curr + 1;
-  const int wd = __float_as_int(nd.w);
-  const int dim = wd & 3;
+  const float4 nd = node1<WIDE>(nodes, w.c1);
+  const uint32_t word = __float_as_uint(nd.w);
+  const uint32_t dim = word & 3u;
   const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
   const float diff = dim == 0 ? dx : (dim == 1 ? dy : dz);   // = q[dim] - nd[dim]
-  const int side = diff > 0.f ? 1 : 0;
-  const int close_c = child + side, far_c = child + 1 - side;
-  const int parent = ((w.curr + 1) >> 1) - 1;
-  const bool down = w.prev < child;
-  const bool test = (down && close_c >= n) || w.prev == close_c;
+  const uint32_t close1 = 2 * w.c1 + (diff > 0.f ? 1u : 0u), far1 = close1 ^ 1u;
+  const bool closeok = close1 <= n;
+  const bool test = w.up || !closeok;
   const float d2 = dx * dx + dy * dy + dz * dz;
-  const double key = key_make(d2, (uint32_t)wd >> 2);
-  const bool cand = w.walking && test && key < list[K - 1];
-  int next, nprev;
-  if (JUMP) {
-    if (down && close_c < n) {
-      next = close_c;
-      nprev = w.curr;
-      w.far_mask &= ~(2u << w.depth);
-      w.depth++;
-    } else if (far_c < n && diff * diff <= w.bound) {
-      next = far_c;
-      nprev = w.curr;
-      w.far_mask |= 2u << w.depth;
-      w.depth++;
-    } else {
-      // curr is finished: deepest close-child ancestor-or-self a (depth da);
-      // bit 0 (the root) is always clear, so da = 0 ends the walk
-      const uint32_t open = (~w.far_mask & ((2u << w.depth) - 1u)) | 1u;
-      const int da = 31 - __clz(open);
-      const int a = ((w.curr + 1) >> (w.depth - da)) - 1;
-      next = da == 0 ? -1 : ((a + 1) >> 1) - 1;
-      nprev = a;
-      w.depth = da - 1;
-    }
-  } else {
-    if (w.prev == far_c) next = parent;
-    else if (w.prev == close_c || close_c >= n) next = (far_c < n && diff * diff <= w.bound) ? far_c : parent;
-    else next = close_c;
-    nprev = w.curr;
-  }
-  lq[w.qn * lstride] = key;
+  const double key = gkey(d2, word);
+  const bool cand = w.walking && test && key < tail;
+  const bool descend = !w.up && closeok;
+  const bool farok = !descend && far1 <= n && diff * diff <= w.bound;
+  const bool stay = descend || farok;
+  const uint32_t j1 = __builtin_ctz(~w.far_mask) + 1;   // far_mask has <= 30 bits: ~far_mask != 0
+  const uint32_t upnode = w.c1 >> j1;                   // 0: the walk is over
+  const uint32_t next = descend ? close1 : (farok ? far1 : upnode);
+  const bool go = w.walking && (stay || upnode != 0);
+  w.far_mask = stay ? (w.far_mask << 1 | (farok ? 1u : 0u)) : w.far_mask >> j1;
+  w.up = !stay;
+  lq[(w.qn + 1) * lstride] = key;
   w.qn += cand ? 1 : 0;
-  const bool go = w.walking && next >= 0;
-  w.prev = go ? nprev : w.prev;
-  w.curr = go ? next : w.curr;
+  w.c1 = go ? next : w.c1;
   w.walking = go;
 }
 
-// Wave-uniform insert round: every lane with a queued key pops one.
+// Wave-uniform insert round: every lane pops one queued key (an empty queue
+// reads slot 0, DBL_MAX); list_insert leaves the list unchanged for a key above
+// its last entry, so the round needs no per-lane branch.
 template <int K>
 __device__ __forceinline__ void lean_round(double (&list)[K], LeanWalk& w, const double* lq, int lstride) {
-  const bool pop = w.qn > 0;
-  w.qn -= pop ? 1 : 0;
-  const double ik = pop ? lq[w.qn * lstride] : __longlong_as_double(0x7FEFFFFFFFFFFFFFll);
-  if (ik < list[K - 1]) {
-    list_insert<K>(list, ik);
-    w.bound = key_d2(list[K - 1]);
-  }
+  const double ik = lq[w.qn * lstride];
+  w.qn = w.qn > 0 ? w.qn - 1 : 0;
+  list_insert<K>(list, ik);
+  w.bound = gkey_d2(list[K - 1]);
 }
 
-__device__ __forceinline__ double lean_sentinel(float cut) {
-  return __longlong_as_double((long long)((((uint64_t)__float_as_uint(cut)) << 32 | 0xFFFFFFFFull) + kKeyBias));
-}
-
-template <int K, int QL, bool JUMP = false>
+template <int K, int QL, bool WIDE>
 __device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float cut, bool valid,
                                               double (&list)[K], double* lq, int lstride) {
-  const double sentinel = lean_sentinel(cut);
+  const double sentinel = gkey(cut, kNoWord);
 #pragma unroll
   for (int j = 0; j < K; j++) list[j] = sentinel;
   if (n <= 0) return;   // empty map: every lane keeps the sentinel list (uniform)
   LeanWalk w;
-  w.start(key_d2(sentinel), valid);
+  w.start(cut, valid);
   w.qn = 0;
+  lq[0] = __longlong_as_double(0x7FEFFFFFFFFFFFFFll);   // slot 0: DBL_MAX, never inserted
   for (;;) {
-    lean_step<K, JUMP>(nodes, n, q, list, w, lq, lstride);
-    const bool any_walking = __ballot(w.walking) != 0;
-    if (__ballot(w.qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
+    lean_step<K, WIDE>(nodes, (uint32_t)n, q, list[K - 1], w, lq, lstride);
+    const bool any_walking = ballot(w.walking) != 0;
+    if (ballot(w.qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
       lean_round<K>(list, w, lq, lstride);
-      if (!any_walking && __ballot(w.qn > 0) == 0) break;
+      if (!any_walking && ballot(w.qn > 0) == 0) break;
     }
   }
-}
-
-// radius^2 of a finished lean list: the K-th d^2, or r2 if the list did not fill
-template <int K>
-__device__ __forceinline__ float radiance_r2(const double (&list)[K], float r2) {
-  return key_id(list[K - 1]) == 0xFFFFFFFFu ? r2 : key_d2(list[K - 1]);
 }
 
 // pm_knn: K-wide list for k <= K; k > 128 runs 128-wide passes (j0 = output
@@ -328,6 +330,22 @@ __device__ __forceinline__ v3 radiance(const double (&list)[kKNearest], const fl
     if (id == 0xFFFFFFFFu) continue;
     const float4 pl = payload[id];
     const float dist = sqrtf(key_d2(list[p]));
+    const float w = 1 - (dist / sqrtf(r2) * kConeFilterC);
+    flux = add(flux, smul(brdf * pl.w * w, v3{pl.x, pl.y, pl.z}));
+  }
+  return divf(flux, (1 - (2.f / 3.f) * (1.f / kConeFilterC)) * 2 * kPI * r2);
+}
+
+// The same over a gather (gkey) list: neighbour id = node word >> 2.
+__device__ __forceinline__ v3 radiance_g(const double (&list)[kKNearest], const float4* __restrict__ payload,
+                                         float brdf, float r2) {
+  v3 flux = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < kKNearest; p++) {
+    const uint32_t word = gkey_word(list[p]);
+    if (word == kNoWord) continue;
+    const float4 pl = payload[word >> 2];
+    const float dist = sqrtf(gkey_d2(list[p]));
     const float w = 1 - (dist / sqrtf(r2) * kConeFilterC);
     flux = add(flux, smul(brdf * pl.w * w, v3{pl.x, pl.y, pl.z}));
   }
@@ -389,11 +407,11 @@ __device__ __forceinline__ float follower_cut(const float4* __restrict__ lead, i
 // from the leaders. TAG only separates the global-map launches into their own
 // kernel symbol (rocprof). perm: lane of walk rank r takes query perm[r] and
 // writes its result there (Morton walk order without permuted copies).
-template <int TAG, bool LEADERS>
+template <int TAG, bool LEADERS, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead) {
-  __shared__ double lq[kGatherQL * 256];
+  __shared__ double lq[(kGatherQL + 1) * 256];
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
   const bool valid = r < nq;
@@ -403,12 +421,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const float R2 = kKMaxDistance * kKMaxDistance;
   const float cut = (valid && !LEADERS) ? follower_cut(lead, nq, r, q, R2) : lean_cut(R2);
   double list[kKNearest];
-  knn_walk_lean<kKNearest, kGatherQL, true>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
+  knn_walk_lean<kKNearest, kGatherQL, WIDE>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
   if (valid) {
-    const bool full = key_id(list[kKNearest - 1]) != 0xFFFFFFFFu;
-    const v3 f = radiance(list, payload, qq.w, full ? key_d2(list[kKNearest - 1]) : R2);
+    const bool full = gkey_word(list[kKNearest - 1]) != kNoWord;
+    const v3 f = radiance_g(list, payload, qq.w, full ? gkey_d2(list[kKNearest - 1]) : R2);
     out[i] = make_float4(f.x, f.y, f.z, 0.f);
-    if (LEADERS) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, full ? key_d2(list[kKNearest - 1]) : -1.f);
+    if (LEADERS) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, full ? gkey_d2(list[kKNearest - 1]) : -1.f);
   }
 }
 
@@ -494,14 +512,24 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   DevBuf<float4> lead(nl);
   if (!lead.p) return hipErrorOutOfMemory;
   const int gl = grid_for(nl, 256), gf = grid_for(nq - nl, 256);
-#define PM_LEVELS(T)                                                                                            \
-  k_gather_level<T, true><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p);          \
+  // node byte offsets fit 32 bits below 2^28 nodes (saddr loads); larger maps use 64-bit addresses
+  const bool wide = n >= (1 << 28);
+#define PM_LEVELS(T, W)                                                                                          \
+  k_gather_level<T, true, W><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p);       \
   PM_HIP_TRY(hipGetLastError());                                                                                \
-  if (nq > nl) k_gather_level<T, false><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p)
+  if (nq > nl) k_gather_level<T, false, W><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p)
   if (tag == 1) {
-    PM_LEVELS(1);
+    if (wide) {
+      PM_LEVELS(1, true);
+    } else {
+      PM_LEVELS(1, false);
+    }
   } else {
-    PM_LEVELS(0);
+    if (wide) {
+      PM_LEVELS(0, true);
+    } else {
+      PM_LEVELS(0, false);
+    }
   }
 #undef PM_LEVELS
   return hipGetLastError();

@@ -23,6 +23,8 @@
 #define R2 1e4f
 #define STRIDE 16
 static int BUCKET = 63;
+// walk rank of follower thread t (the production follower launch skips the leaders)
+#define FRANK(t) (((t) / (STRIDE - 1)) * STRIDE + 1 + (t) % (STRIDE - 1))
 
 typedef struct { float p[3]; int id, dim; } Node;
 static float* P;
@@ -104,6 +106,55 @@ static float bound_of(const List* L, float cut) { return L->n < K ? cut : key_d2
 static float dist2(const float* q, const Node* nd) {
   const float dx = q[0] - nd->p[0], dy = q[1] - nd->p[1], dz = q[2] - nd->p[2];
   return dx * dx + dy * dy + dz * dz;
+}
+
+// ---- kk nearest point ids of q (kk <= 256), sorted by (d2, id): leader lists for the Y model
+static uint64_t GK[256];
+static int GN, GKK;
+static void gk_visit(const float* q, int t) {
+  if (t >= N) return;
+  const Node* nd = &T[t];
+  const float diff = q[nd->dim] - nd->p[nd->dim];
+  const int side = diff > 0.f;
+  gk_visit(q, 2 * t + 1 + side);
+  const uint64_t k = mkkey(dist2(q, nd), nd->id);
+  if (GN < GKK || k < GK[GKK - 1]) {
+    int j = GN < GKK ? GN++ : GKK - 1;
+    while (j > 0 && GK[j - 1] > k) { GK[j] = GK[j - 1]; j--; }
+    GK[j] = k;
+  }
+  const float b = GN < GKK ? 1e30f : key_d2(GK[GKK - 1]);
+  if (diff * diff <= b) gk_visit(q, 2 * t + 2 - side);
+}
+static int knn_ids(const float* q, int kk, int* ids) {
+  GN = 0; GKK = kk;
+  gk_visit(q, 0);
+  for (int i = 0; i < GN; i++) ids[i] = (int)(uint32_t)GK[i];
+  return GN;
+}
+static int cmp_fl(const void* a, const void* b) {
+  const float x = *(const float*)a, y = *(const float*)b;
+  return x < y ? -1 : x > y;
+}
+// 50th smallest d2 from q over the distinct points of the given id sets
+static float kth_of_sets(const float* q, int** sets, const int* ns, int nsets) {
+  static float d[1024];
+  static int seen[1024];
+  int m = 0;
+  for (int s = 0; s < nsets; s++)
+    for (int i = 0; i < ns[s]; i++) {
+      const int id = sets[s][i];
+      int dup = 0;
+      for (int j = 0; j < m && !dup; j++) dup = seen[j] == id;
+      if (dup) continue;
+      seen[m] = id;
+      const float* p = &P[3 * id];
+      const float dx = q[0] - p[0], dy = q[1] - p[1], dz = q[2] - p[2];
+      d[m++] = dx * dx + dy * dy + dz * dz;
+    }
+  if (m < K) return 1e30f;
+  qsort(d, m, sizeof(float), cmp_fl);
+  return d[K - 1];
 }
 
 // ---- A: per-lane JUMP walk (lean_step), returns node loads; counts inserts
@@ -282,6 +333,87 @@ static int cmp_f(const void* a, const void* b) {
   const float x = *(const float*)a, y = *(const float*)b;
   return x < y ? -1 : x > y;
 }
+// ---- G: lockstep wave with bucketed bottoms: nodes at depth >= DB are never
+// walked; a walk that would enter a depth-DB node scans its whole subtree (<= 7
+// nodes: levels DB..DB+2) in one iteration, testing every point. Rounds pop one
+// queued key per lane when some lane holds >= QG - 7 keys (room for one scan).
+// Cost model (VALU instructions): walk step WS, scan SC, round RC; a wave
+// iteration costs WS if any lane walks plus SC if any lane scans.
+static int DB;
+static double g_cost(const float* const* qs, const float* cuts, int QG, double WS, double SC, double RC, int* iters,
+                     int* rounds) {
+  Lane ln[64];
+  int scan_root[64];
+  for (int l = 0; l < 64; l++) {
+    ln[l].q = qs[l]; ln[l].cut = cuts[l]; ln[l].bound = cuts[l]; list_init(&ln[l].L);
+    ln[l].prev = -1; ln[l].curr = 0; ln[l].depth = 0; ln[l].walking = 1; ln[l].qn = 0; ln[l].far_mask = 0;
+    scan_root[l] = -1;
+  }
+  double cost = 0;
+  *iters = 0; *rounds = 0;
+  for (;;) {
+    int any_walk = 0, any_scan = 0, any_live = 0;
+    for (int l = 0; l < 64; l++) {
+      Lane* w = &ln[l];
+      if (!w->walking) continue;
+      any_live = 1;
+      if (scan_root[l] >= 0) {   // scan the bucket under scan_root, then return to its parent
+        any_scan = 1;
+        const int t = scan_root[l];
+        for (int lev = 0; lev < 3; lev++)
+          for (int j = 0; j < (1 << lev); j++) {
+            const long c = (long)(t + 1) * (1 << lev) - 1 + j;
+            if (c >= N) continue;
+            const float d2 = dist2(w->q, &T[c]);
+            const uint64_t k = mkkey(d2, T[c].id);
+            if (d2 <= w->cut && (w->L.n < K || k < w->L.key[K - 1])) w->qk[w->qn++] = k;
+          }
+        scan_root[l] = -1;
+        w->prev = t;   // back at the parent (curr), arrived from child t
+        continue;
+      }
+      any_walk = 1;
+      const Node* nd = &T[w->curr];
+      const int child = 2 * w->curr + 1;
+      const float diff = w->q[nd->dim] - nd->p[nd->dim];
+      const int side = diff > 0.f, close = child + side, far = child + 1 - side;
+      const int down = w->prev < child;
+      if ((down && close >= N) || w->prev == close) {
+        const float d2 = dist2(w->q, nd);
+        const uint64_t k = mkkey(d2, nd->id);
+        if (d2 <= w->cut && (w->L.n < K || k < w->L.key[K - 1])) w->qk[w->qn++] = k;
+      }
+      int next;
+      if (w->prev == far) next = ((w->curr + 1) >> 1) - 1;
+      else if (w->prev == close || close >= N) next = (far < N && diff * diff <= w->bound) ? far : ((w->curr + 1) >> 1) - 1;
+      else next = close;
+      if (next < 0) { w->walking = 0; continue; }
+      if (next > w->curr && 31 - __builtin_clz((uint32_t)next + 1) >= DB) { scan_root[l] = next; continue; }
+      w->prev = w->curr; w->curr = next;
+    }
+    if (!any_live) break;
+    (*iters)++;
+    cost += (any_walk ? WS : 0) + (any_scan ? SC : 0);
+    int need = 0, left = 0, live = 0;
+    for (int l = 0; l < 64; l++) { need |= ln[l].qn >= QG - 7; live |= ln[l].walking; }
+    if (need || !live) {
+      do {
+        (*rounds)++;
+        cost += RC;
+        left = 0;
+        need = 0;
+        for (int l = 0; l < 64; l++) {
+          Lane* w = &ln[l];
+          if (w->qn > 0) { list_insert(&w->L, w->qk[--w->qn]); w->bound = bound_of(&w->L, w->cut); }
+          left |= w->qn > 0;
+          need |= w->qn >= QG - 7;
+        }
+      } while ((!live && left) || need);
+    }
+  }
+  return cost;
+}
+
 static void regroup_model(const float* Q, const int* ord, long nq, const float* lt, long nl, int blocks) {
   double morton = 0, sorted = 0, mean = 0;
   List L;
@@ -347,6 +479,7 @@ int main(int argc, char** argv) {
   int* v = malloc(sizeof(int) * (size_t)N);
   for (int i = 0; i < N; i++) v[i] = i;
   build(0, v, N);
+  { int dm = 0; while ((2L << dm) - 1 < N) dm++; DB = dm - 2; }   // deepest level dm (0-based)
   // Morton order of the queries over their bounds (30-bit)
   float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
   for (long i = 0; i < nq; i++)
@@ -363,7 +496,7 @@ int main(int argc, char** argv) {
     ord[i] = (int)i;
   }
   qsort(ord, (size_t)nq, sizeof(int), cmp_mk);
-  const long nwaves = nq / 64;
+  const long nwaves = (nq - nq / STRIDE) / 64 - 1;
   // leader records (every STRIDE-th query in walk order, plain cut-off)
   const long nl = (nq + STRIDE - 1) / STRIDE;
   float* lt = malloc(sizeof(float) * (size_t)nl);
@@ -376,8 +509,8 @@ int main(int argc, char** argv) {
   char* need = calloc((size_t)nl, 1);
   const int regroup_blocks = argc > 6 ? atoi(argv[6]) : 0;
   for (int s = 0; s < sample; s++) {
-    const long r0 = waves[s] * 64;
-    for (long r = r0 - 2 * STRIDE; r < r0 + 64 + 3 * STRIDE; r += STRIDE)
+    const long r0 = FRANK(waves[s] * 64);
+    for (long r = r0 - 2 * STRIDE; r < r0 + 80 + 3 * STRIDE; r += STRIDE)
       if (r >= 0 && r / STRIDE < nl) need[r / STRIDE] = 1;
   }
   for (long j = 0; j < nl; j++) {
@@ -388,14 +521,19 @@ int main(int argc, char** argv) {
   }
   double a_mean = 0, a_max = 0, a_ins = 0, b_nodes = 0, b_ins = 0, c_nodes = 0, c_buckets = 0, c_pts = 0, c_ins = 0;
   double e_nodes = 0, e_buckets = 0, e_pts = 0, e_ins = 0, e_max_nodes = 0, e_max_pts = 0, e_max_cost = 0;
+  double y_it[8] = {0}, y_rounds[8] = {0}, y_ratio[8] = {0}, y_n[8] = {0}, s_ratio = 0, s_n = 0;
+  double z_it[3] = {0}, z_rd[3] = {0}, z_ratio[3] = {0}, z_n[3] = {0};
+  double g_c[2] = {0}, g_it[2] = {0}, g_rd[2] = {0}, d_c[2] = {0};
+  double x_it[4] = {0, 0, 0, 0}, x_rounds[4] = {0, 0, 0, 0};
   double a_plain_max = 0, b_plain = 0, c_maxins = 0, b_maxins = 0, d_it[2] = {0, 0}, d_rounds[2] = {0, 0}, d_ins[2] = {0, 0};
   for (int s = 0; s < sample; s++) {
-    const long r0 = waves[s] * 64;
+    const long t0 = waves[s] * 64;
     Packet W, Wp, Wc;
+    float exact[64];
     memset(&W, 0, sizeof(W));
     int mx = 0, mxp = 0, ins = 0;
     for (int l = 0; l < 64; l++) {
-      const long r = r0 + l;
+      const long r = FRANK(t0 + l);
       const float* q = &Q[3 * ord[r]];
       float cut = nextafterf(R2, 0.f);
       if (r % STRIDE) {
@@ -411,10 +549,96 @@ int main(int argc, char** argv) {
       int d2 = 0;
       const int sp = walk_lane(q, nextafterf(R2, 0.f), &L, &d2);
       if (sp > mxp) mxp = sp;
+      exact[l] = L.n >= K ? key_d2(L.key[K - 1]) : nextafterf(R2, 0.f);
       W.q[l] = q;
       W.cut[l] = cut;
     }
     W.n = 64;
+    {   // Y: cut from the leaders' kk-lists (50th smallest d2 over their points)
+      static const int kks[4] = {50, 64, 96, 128};
+      for (int v = 0; v < 8; v++) {
+        const int kk = kks[v & 3], two = v >> 2;
+        float yc[64];
+        for (int l = 0; l < 64; l++) {
+          const long r = FRANK(t0 + l);
+          yc[l] = W.cut[l];
+          if (r % STRIDE == 0) continue;
+          const long ja = r / STRIDE, jb = ja + 1;
+          static int ia[256], ib[256];
+          int* sets[2] = {ia, ib};
+          int ns[2];
+          const float* qa = &Q[3 * ord[ja * STRIDE]];
+          const float* qb = jb * STRIDE < nq ? &Q[3 * ord[jb * STRIDE]] : qa;
+          const float* q = W.q[l];
+          const float da = dist2(q, &(Node){{qa[0], qa[1], qa[2]}, 0, 0});
+          const float db = dist2(q, &(Node){{qb[0], qb[1], qb[2]}, 0, 0});
+          ns[0] = knn_ids(two || da <= db ? qa : qb, kk, ia);
+          ns[1] = two ? knn_ids(qb, kk, ib) : 0;
+          const float b = kth_of_sets(q, sets, ns, two ? 2 : 1) * (1.f + 1e-6f);
+          if (b < yc[l]) yc[l] = b;
+          y_ratio[v] += yc[l] / exact[l];
+          y_n[v]++;
+        }
+        int rounds = 0;
+        long li = 0;
+        y_it[v] += wave_lockstep(W.q, yc, 0, &rounds, &li);
+        y_rounds[v] += rounds;
+      }
+      for (int l = 0; l < 64; l++) if (FRANK(t0 + l) % STRIDE) { s_ratio += W.cut[l] / exact[l]; s_n++; }
+    }
+    for (int v = 0; v < 3; v++) {   // Z: cut from q's own depth-(Dmax - h) subtree (50th smallest d2 of its points)
+      const int h = 5 + v;   // subtree of 2^(h+1)-1 nodes
+      float zc[64];
+      for (int l = 0; l < 64; l++) {
+        const float* q = W.q[l];
+        zc[l] = W.cut[l];
+        int t = 0, dep = 0;
+        while (dep < DB + 2 - h) {   // close-path descent
+          const Node* nd = &T[t];
+          const float diff = q[nd->dim] - nd->p[nd->dim];
+          const int c = 2 * t + 1 + (diff > 0.f);
+          if (c >= N) break;
+          t = c; dep++;
+        }
+        static float d[1024];
+        int m = 0;
+        for (int lev = 0; lev <= h; lev++)
+          for (long j = 0; j < (1L << lev); j++) {
+            const long c = (long)(t + 1) * (1L << lev) - 1 + j;
+            if (c < N) d[m++] = dist2(q, &T[c]);
+          }
+        if (m >= K) {
+          qsort(d, m, sizeof(float), cmp_fl);
+          const float b = d[K - 1] * (1.f + 1e-6f);
+          if (b < zc[l]) zc[l] = b;
+        }
+        z_ratio[v] += zc[l] / exact[l];
+        z_n[v]++;
+      }
+      int rounds = 0;
+      long li = 0;
+      z_it[v] += wave_lockstep(W.q, zc, 0, &rounds, &li);
+      z_rd[v] += rounds;
+    }
+    for (int v = 0; v < 2; v++) {   // G: bucketed-bottom lockstep, seeded / exact cut
+      float gc[64];
+      for (int l = 0; l < 64; l++) gc[l] = v ? fminf(exact[l] * (1.f + 1e-6f), W.cut[l]) : W.cut[l];
+      int it, rd;
+      g_c[v] += g_cost(W.q, gc, 16, 50, 84, 111, &it, &rd);
+      g_it[v] += it; g_rd[v] += rd;
+      int it2, rd2;
+      d_c[v] += wave_lockstep(W.q, gc, 0, &rd2, &(long){0}) * 60.0;
+      d_c[v] += rd2 * 111.0;
+    }
+    for (int f = 0; f < 4; f++) {   // X: lockstep with cut = exact k-th d2 x factor
+      static const float fac[4] = {1.0f, 1.15f, 1.5f, 2.0f};
+      float xc[64];
+      for (int l = 0; l < 64; l++) xc[l] = fminf(exact[l] * fac[f] * (1.f + 1e-6f), W.cut[l]);
+      int rounds = 0;
+      long li = 0;
+      x_it[f] += wave_lockstep(W.q, xc, 0, &rounds, &li);
+      x_rounds[f] += rounds;
+    }
     for (int pol = 0; pol < 2; pol++) {
       int rounds = 0;
       long li = 0;
@@ -486,5 +710,18 @@ int main(int argc, char** argv) {
   for (int pol = 0; pol < 2; pol++)
     printf("D lockstep wave (QL %d, %s rounds): iterations %.1f, rounds %.1f, inserts/lane %.1f\n", QL,
            pol ? "batch-merge" : "pop-one", d_it[pol] / S, d_rounds[pol] / S, d_ins[pol] / S / 64);
+  for (int v = 0; v < 3; v++)
+    printf("Z own subtree of %d nodes: cut/exact mean %.3f, iterations %.1f, rounds %.1f, VALU %.0f\n",
+           (2 << (5 + v)) - 1, z_ratio[v] / z_n[v], z_it[v] / S, z_rd[v] / S, (z_it[v] * 60 + z_rd[v] * 111) / S);
+  for (int v = 0; v < 2; v++)
+    printf("G bucketed bottom (DB %d), %s cut: iterations %.1f, rounds %.1f, VALU %.0f vs current walk %.0f\n", DB,
+           v ? "exact" : "seeded", g_it[v] / S, g_rd[v] / S, g_c[v] / S, d_c[v] / S);
+  printf("seeded (triangle) cut / exact k-th d2: mean %.3f\n", s_ratio / s_n);
+  for (int v = 0; v < 8; v++)
+    printf("Y %s leader list kk=%d: cut/exact mean %.3f, iterations %.1f, rounds %.1f\n", v >> 2 ? "two" : "nearest",
+           (int[]){50, 64, 96, 128}[v & 3], y_ratio[v] / y_n[v], y_it[v] / S, y_rounds[v] / S);
+  for (int f = 0; f < 4; f++)
+    printf("X lockstep, cut = min(seeded, exact k-th d2 x %.2f): iterations %.1f, rounds %.1f\n",
+           (double)(f == 0 ? 1.0f : f == 1 ? 1.15f : f == 2 ? 1.5f : 2.0f), x_it[f] / S, x_rounds[f] / S);
   return 0;
 }
