@@ -228,8 +228,10 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_bal
 //    (arriving from the close child a), or stop when a is the root.
 template <int K, bool WIDE>
 __device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, uint32_t n, v3 q, double tail,
-                                          LeanWalk& w, double* lq, int lstride) {
-  const float4 nd = node1<WIDE>(nodes, w.c1);
+                                          LeanWalk& w, float4& nd, double* lq, int lstride) {
+  // software-pipelined: `nd` (node c1) was loaded by the previous step; the
+  // transitions come first, so the next node's load is issued before the point
+  // test, the queue write and any insert round of this step
   const uint32_t word = __float_as_uint(nd.w);
   const uint32_t dim = word & 3u;
   const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
@@ -237,9 +239,6 @@ __device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, uint
   const uint32_t close1 = 2 * w.c1 + (diff > 0.f ? 1u : 0u), far1 = close1 ^ 1u;
   const bool closeok = close1 <= n;
   const bool test = w.up || !closeok;
-  const float d2 = dx * dx + dy * dy + dz * dz;
-  const double key = gkey(d2, word);
-  const bool cand = w.walking && test && key < tail;
   const bool descend = !w.up && closeok;
   const bool farok = !descend && far1 <= n && diff * diff <= w.bound;
   const bool stay = descend || farok;
@@ -247,12 +246,18 @@ __device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, uint
   const uint32_t upnode = w.c1 >> j1;                   // 0: the walk is over
   const uint32_t next = descend ? close1 : (farok ? far1 : upnode);
   const bool go = w.walking && (stay || upnode != 0);
+  const uint32_t c1n = go ? next : w.c1;
+  const float4 ndn = node1<WIDE>(nodes, c1n);
+  const float d2 = dx * dx + dy * dy + dz * dz;
+  const double key = gkey(d2, word);
+  const bool cand = w.walking && test && key < tail;
   w.far_mask = stay ? (w.far_mask << 1 | (farok ? 1u : 0u)) : w.far_mask >> j1;
   w.up = !stay;
   lq[(w.qn + 1) * lstride] = key;
   w.qn += cand ? 1 : 0;
-  w.c1 = go ? next : w.c1;
+  w.c1 = c1n;
   w.walking = go;
+  nd = ndn;
 }
 
 // Wave-uniform insert round: every lane pops one queued key (an empty queue
@@ -277,8 +282,9 @@ __device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, 
   w.start(cut, valid);
   w.qn = 0;
   lq[0] = __longlong_as_double(0x7FEFFFFFFFFFFFFFll);   // slot 0: DBL_MAX, never inserted
+  float4 nd = node1<WIDE>(nodes, 1);
   for (;;) {
-    lean_step<K, WIDE>(nodes, (uint32_t)n, q, list[K - 1], w, lq, lstride);
+    lean_step<K, WIDE>(nodes, (uint32_t)n, q, list[K - 1], w, nd, lq, lstride);
     const bool any_walking = ballot(w.walking) != 0;
     if (ballot(w.qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
       lean_round<K>(list, w, lq, lstride);
