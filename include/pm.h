@@ -119,9 +119,10 @@ const char* pm_status_string(int status);
 /* Number of visible HIP devices (0 on a host without a GPU; never fails). */
 int pm_device_count(int32_t* count);
 /* Microseconds of the last kernel(s) of a phase, measured with hipEvents on
- * the stream the kernels ran on. phase: 0 trace, 1 compaction, 2 kd-build,
- * 3 render-paths, 4 knn-gather (all), 5 resolve, 6 bvh-build, 7 the global-map
- * gather launch alone (the dominant kernel). */
+ * the stream the kernels ran on, as seen by the calling host thread (each
+ * thread reads the phases of its own last calls). phase: 0 trace, 1
+ * compaction, 2 kd-build, 3 render-paths, 4 knn-gather (all), 5 resolve, 6
+ * bvh-build, 7 the global-map gather launch alone (the dominant kernel). */
 int pm_last_phase_us(int32_t phase, double* us);
 /* Device memory for callers without HIP headers (the CLI, cgo / JNI / ctypes
  * bindings): hipMalloc / hipFree / synchronous hipMemcpy on the current device. */

@@ -50,17 +50,17 @@ bool render_job_finished(const pm_render_job* J);
 void render_job_mark_finished(pm_render_job* J);
 
 namespace {
-std::mutex g_phase_mu;
-double g_phase_us[PH_COUNT] = {0};
+std::mutex g_phase_mu;   // guards g_render_stats
+// phase timers are per host thread: a caller that drives two streams from two
+// threads (the caustic pass beside the global trace) reads each call's own time
+thread_local double g_phase_us[PH_COUNT] = {0};
 pm_render_stats g_render_stats{};
 }  // namespace
 
 void record_phase_us(int phase, double us) {
-  std::lock_guard<std::mutex> lk(g_phase_mu);
   if (phase >= 0 && phase < PH_COUNT) g_phase_us[phase] += us;
 }
 static void reset_phase(int phase) {
-  std::lock_guard<std::mutex> lk(g_phase_mu);
   if (phase >= 0 && phase < PH_COUNT) g_phase_us[phase] = 0;
 }
 
@@ -153,7 +153,6 @@ int pm_device_count(int32_t* count) {
 
 int pm_last_phase_us(int32_t phase, double* us) {
   if (!us || phase < 0 || phase >= PH_COUNT) return PM_ERR_INVALID;
-  std::lock_guard<std::mutex> lk(g_phase_mu);
   *us = g_phase_us[phase];
   return PM_OK;
 }

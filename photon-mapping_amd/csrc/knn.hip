@@ -199,12 +199,22 @@ struct LeanWalk {
   bool up;             // arrived at c1 from its close child: its point test is due
   bool walking;
   int qn;              // queued candidates in this lane's LDS column (slots 1..QL; slot 0 = DBL_MAX)
+  // JUMP target of the current state, computed when the state is set (off the
+  // node-load critical path): a = c1 >> (j1 - 1) with j1 - 1 the lowest clear
+  // bit of far_mask is the deepest close-child ancestor-or-self; upnode = its
+  // parent c1 >> j1 (0: a is the root, the walk is over)
+  uint32_t j1, upnode;
+  __device__ __forceinline__ void set_jump() {
+    j1 = __builtin_ctz(~far_mask) + 1;   // far_mask has <= 30 bits: ~far_mask != 0
+    upnode = c1 >> j1;
+  }
   __device__ __forceinline__ void start(float b, bool valid) {
     bound = b;
     c1 = 1;
     far_mask = 0;   // the root's bit stays 0: a jump that reaches it ends the walk
     up = false;
     walking = valid;
+    set_jump();
   }
 };
 
@@ -223,9 +233,8 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_bal
 // Transitions (all computed, one selected):
 //  - descend to the close child (arrived from the parent and it exists);
 //  - else enter the far child if it exists and the plane is within the bound;
-//  - else JUMP: a = c1 >> j with j the lowest clear bit of far_mask is the
-//    deepest close-child ancestor-or-self; go to its parent c1 >> (j + 1)
-//    (arriving from the close child a), or stop when a is the root.
+//  - else JUMP to LeanWalk::upnode (arriving from its close child), or stop
+//    when that is 0.
 template <int K, bool WIDE>
 __device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, uint32_t n, v3 q, double tail,
                                           LeanWalk& w, float4& nd, double* lq, int lstride) {
@@ -242,21 +251,20 @@ __device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, uint
   const bool descend = !w.up && closeok;
   const bool farok = !descend && far1 <= n && diff * diff <= w.bound;
   const bool stay = descend || farok;
-  const uint32_t j1 = __builtin_ctz(~w.far_mask) + 1;   // far_mask has <= 30 bits: ~far_mask != 0
-  const uint32_t upnode = w.c1 >> j1;                   // 0: the walk is over
-  const uint32_t next = descend ? close1 : (farok ? far1 : upnode);
-  const bool go = w.walking && (stay || upnode != 0);
+  const uint32_t next = descend ? close1 : (farok ? far1 : w.upnode);
+  const bool go = w.walking && (stay || w.upnode != 0);
   const uint32_t c1n = go ? next : w.c1;
   const float4 ndn = node1<WIDE>(nodes, c1n);
   const float d2 = dx * dx + dy * dy + dz * dz;
   const double key = gkey(d2, word);
   const bool cand = w.walking && test && key < tail;
-  w.far_mask = stay ? (w.far_mask << 1 | (farok ? 1u : 0u)) : w.far_mask >> j1;
+  w.far_mask = stay ? (w.far_mask << 1 | (farok ? 1u : 0u)) : w.far_mask >> w.j1;
   w.up = !stay;
   lq[(w.qn + 1) * lstride] = key;
   w.qn += cand ? 1 : 0;
   w.c1 = c1n;
   w.walking = go;
+  w.set_jump();
   nd = ndn;
 }
 
