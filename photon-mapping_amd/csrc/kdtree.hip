@@ -385,25 +385,30 @@ __device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, uint64_t* sh) {
 
 // Per-tile segmented aggregate: the (L, R) counts of the positions at or after
 // the last subtree start inside the tile (all positions if none starts in it),
-// and whether one starts -- a plain block sum, no scan.
-__global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void k_kd_count(KdLists Lst, int64_t n,
+// and whether one starts -- a plain wave sum, no scan. One wave per tile (the
+// tile's positions striped over its 64 lanes): the pass is bound by each
+// tile's dependent loads (tile -> subtree records -> split coordinates), so
+// small blocks keep 4x more tiles in flight than a 256-thread tile did.
+constexpr int kCountThreads = 64;
+constexpr int kCountIPT = kPartTile / kCountThreads;
+__global__ __launch_bounds__(kCountThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void k_kd_count(KdLists Lst, int64_t n,
                                                            SegTab T, int level,
                                                            const int32_t* __restrict__ tile_seg,
                                                            SegVal* __restrict__ tile_agg) {
   __shared__ SegRec cache[kSegCache];
-  __shared__ uint64_t sh[kPartThreads / 64];
   const TileSegs ts = tile_segs(T, level, tile_seg, cache);
   const int64_t base = (int64_t)blockIdx.x * kPartTile + threadIdx.x;
   uint64_t sum = 0;
   float4 dummy[3];
 #pragma unroll
-  for (int k = 0; k < kPartIPT; k++) {
+  for (int k = 0; k < kCountIPT; k++) {
     PartItem it;
-    const int64_t p = base + k * kPartThreads;
+    const int64_t p = base + k * kCountThreads;
     part_load<false>(Lst, n, T, level, ts, cache, p, it, dummy);
     if (p >= ts.last_start) sum += pack_cls(it);
   }
-  sum = block_sum_u64(sum, sh);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
   if (threadIdx.x == 0) {
     SegVal agg;
 #pragma unroll
@@ -786,7 +791,7 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
     if (L == H - 1) break;   // last level: every remaining subtree has one node
     k_kd_tileseg<<<grid_for(ntiles + 1, 256), 256, 0, s>>>(tb.p, L, ntiles, tile_seg.p);
     PM_HIP_TRY(hipGetLastError());
-    k_kd_count<<<(int)ntiles, kPartThreads, 0, s>>>(Lst, n, T, L, tile_seg.p, tagg.p);
+    k_kd_count<<<(int)ntiles, kCountThreads, 0, s>>>(Lst, n, T, L, tile_seg.p, tagg.p);
     PM_HIP_TRY(hipGetLastError());
     k_kd_chunkscan<<<nchunks, kChunk, 0, s>>>(tagg.p, ntiles, tcarry.p, ccarry.p);
     PM_HIP_TRY(hipGetLastError());

@@ -383,9 +383,18 @@ __device__ __forceinline__ v3 radiance_g(const double (&list)[kKNearest], const 
 // 8/4 50.3, 4/2 52.2, 16/2 50.6, 16/4 49.8; leader hierarchies, XCD-contiguous
 // block ranges, pooled lanes, child-line prefetch and deeper queues measured
 // slower; the exact-cut re-walk floor was 34.4 ms.
-constexpr int kSeedStride = 16;
-constexpr int kSeedLeaders = 4;
-constexpr int kGatherQL = 8;   // LDS insert-queue depth
+#ifndef PM_SEED_STRIDE
+#define PM_SEED_STRIDE 16
+#endif
+#ifndef PM_SEED_LEADERS
+#define PM_SEED_LEADERS 4
+#endif
+#ifndef PM_GATHER_QL
+#define PM_GATHER_QL 8
+#endif
+constexpr int kSeedStride = PM_SEED_STRIDE;
+constexpr int kSeedLeaders = PM_SEED_LEADERS;
+constexpr int kGatherQL = PM_GATHER_QL;   // LDS insert-queue depth
 
 __device__ __forceinline__ double seed_bound(float4 lead, v3 q) {
   if (!(lead.w >= 0.f)) return 1e300;
