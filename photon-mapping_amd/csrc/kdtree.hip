@@ -152,12 +152,16 @@ __device__ __forceinline__ int kd_class(const float4 e, int dim, float nc, int n
 #ifndef PM_KD_COUNT_WAVES
 #define PM_KD_COUNT_WAVES 0
 #endif
-constexpr int kPartThreads = 256;
-// positions per thread (tile = 256 * IPT). Config 3 kd build (AoS lists, round
-// 1): IPT 4 44.5 ms (count 114 / part 142 VGPRs), IPT 2 36.4 ms (58 / 92), IPT 1 36.6 ms
+// threads of a partition block; the tile is PM_KD_IPT positions per thread
+// (config 3 kd build, AoS lists, round 1: 256 x 4 44.5 ms (count 114 / part 142
+// VGPRs), 256 x 2 36.4 ms (58 / 92), 256 x 1 36.6 ms)
+#ifndef PM_KD_PART_THREADS
+#define PM_KD_PART_THREADS 256
+#endif
 #ifndef PM_KD_IPT
 #define PM_KD_IPT 2
 #endif
+constexpr int kPartThreads = PM_KD_PART_THREADS;
 constexpr int kPartIPT = PM_KD_IPT;
 constexpr int kPartTile = kPartThreads * kPartIPT;   // positions per tile
 static_assert(kPartTile < 1024, "tile-local counts are packed in 10-bit fields (pack_cls)");
@@ -391,6 +395,7 @@ __device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, uint64_t* sh) {
 // small blocks keep 4x more tiles in flight than a 256-thread tile did.
 constexpr int kCountThreads = 64;
 constexpr int kCountIPT = kPartTile / kCountThreads;
+static_assert(kPartTile % kCountThreads == 0, "count tiles are striped over one wave");
 __global__ __launch_bounds__(kCountThreads) PM_WAVES_ATTR(PM_KD_COUNT_WAVES) void k_kd_count(KdLists Lst, int64_t n,
                                                            SegTab T, int level,
                                                            const int32_t* __restrict__ tile_seg,

@@ -294,10 +294,17 @@ static int wave_lockstep(const float* const* qs, const float* cuts, int policy, 
       int left = 0;
       for (int l = 0; l < 64; l++) {
         Lane* w = &ln[l];
-        const int take = policy ? w->qn : (w->qn > 0);
-        for (int t = 0; t < take; t++) {
-          const uint64_t k = w->qk[--w->qn];
-          if (list_insert(&w->L, k)) (*lane_ins)++;
+        if (policy == 2) {   // filtered pop: skip queued keys the list has outgrown
+          while (w->qn > 0) {
+            const uint64_t k = w->qk[--w->qn];
+            if (list_insert(&w->L, k)) { (*lane_ins)++; break; }
+          }
+        } else {
+          const int take = policy ? w->qn : (w->qn > 0);
+          for (int t = 0; t < take; t++) {
+            const uint64_t k = w->qk[--w->qn];
+            if (list_insert(&w->L, k)) (*lane_ins)++;
+          }
         }
         w->bound = bound_of(&w->L, w->cut);
         left |= w->qn > 0;
@@ -325,6 +332,75 @@ static double seed_bound(const float* lq, float lt, const float* q) {
   const double dx = (double)q[0] - lq[0], dy = (double)q[1] - lq[1], dz = (double)q[2] - lq[2];
   const double c = (sqrt((double)lt) + sqrt(dx * dx + dy * dy + dz * dz)) * (1.0 + 1e-6);
   return c * c * (1.0 + 1e-5) + 1e-30;
+}
+
+// ---- P: pooled lanes: a wave owns NPQ Morton-consecutive followers; a lane
+// whose walk is over and whose queue is empty takes the next one (refill when
+// >= REFILL lanes wait, or every lane waits). Rounds as in D (pop one when a
+// queue is full or no lane walks). Returns iterations; *rounds.
+static int pool_lockstep(const float* const* qs, const float* cuts, int nq, int refill, int* rounds) {
+  Lane ln[64];
+  int next = 0;
+  for (int l = 0; l < 64; l++) { ln[l].walking = 0; ln[l].qn = 0; }
+  int it = 0;
+  *rounds = 0;
+  for (;;) {
+    int idle = 0;
+    for (int l = 0; l < 64; l++) idle += !ln[l].walking && ln[l].qn == 0;
+    if (next < nq && (idle >= refill || idle == 64)) {
+      for (int l = 0; l < 64 && next < nq; l++) {
+        Lane* w = &ln[l];
+        if (w->walking || w->qn) continue;
+        w->q = qs[next]; w->cut = cuts[next]; w->bound = cuts[next]; next++;
+        list_init(&w->L); w->prev = -1; w->curr = 0; w->depth = 0; w->walking = 1; w->far_mask = 0;
+      }
+    }
+    int any = 0;
+    for (int l = 0; l < 64; l++) any |= ln[l].walking || ln[l].qn;
+    if (!any && next >= nq) break;
+    it++;
+    for (int l = 0; l < 64; l++) {
+      Lane* w = &ln[l];
+      if (!w->walking) continue;
+      const Node* nd = &T[w->curr];
+      const int child = 2 * w->curr + 1;
+      const float diff = w->q[nd->dim] - nd->p[nd->dim];
+      const int side = diff > 0.f, close = child + side, far = child + 1 - side;
+      const int down = w->prev < child;
+      if ((down && close >= N) || w->prev == close) {
+        const float d2 = dist2(w->q, nd);
+        const uint64_t k = mkkey(d2, nd->id);
+        if (d2 <= w->cut && (w->L.n < K || k < w->L.key[K - 1])) w->qk[w->qn++] = k;
+      }
+      int nx, nprev;
+      if (down && close < N) { nx = close; nprev = w->curr; w->far_mask &= ~(2u << w->depth); w->depth++; }
+      else if (far < N && diff * diff <= w->bound) { nx = far; nprev = w->curr; w->far_mask |= 2u << w->depth; w->depth++; }
+      else {
+        const uint32_t open = (~w->far_mask & ((2u << w->depth) - 1u)) | 1u;
+        int da = 31;
+        while (!(open >> da & 1)) da--;
+        const int a = ((w->curr + 1) >> (w->depth - da)) - 1;
+        nx = da == 0 ? -1 : ((a + 1) >> 1) - 1;
+        nprev = a;
+        w->depth = da - 1;
+      }
+      if (nx < 0) w->walking = 0; else { w->prev = nprev; w->curr = nx; }
+    }
+    int full = 0, walk = 0;
+    for (int l = 0; l < 64; l++) { full |= ln[l].qn == QL; walk |= ln[l].walking; }
+    // a lane whose walk is over drains its queue in the rounds the others trigger,
+    // or in rounds of its own once no lane walks
+    int pend = 0;
+    for (int l = 0; l < 64; l++) pend += !ln[l].walking && ln[l].qn;
+    if (full || !walk || pend >= refill) {
+      (*rounds)++;
+      for (int l = 0; l < 64; l++) {
+        Lane* w = &ln[l];
+        if (w->qn > 0) { list_insert(&w->L, w->qk[--w->qn]); w->bound = bound_of(&w->L, w->cut); }
+      }
+    }
+  }
+  return it;
 }
 
 // ---- F: wave max steps when the followers of each 256-query block are
@@ -521,11 +597,12 @@ int main(int argc, char** argv) {
   }
   double a_mean = 0, a_max = 0, a_ins = 0, b_nodes = 0, b_ins = 0, c_nodes = 0, c_buckets = 0, c_pts = 0, c_ins = 0;
   double e_nodes = 0, e_buckets = 0, e_pts = 0, e_ins = 0, e_max_nodes = 0, e_max_pts = 0, e_max_cost = 0;
+  double pit_static = 0, prd_static = 0;
   double y_it[8] = {0}, y_rounds[8] = {0}, y_ratio[8] = {0}, y_n[8] = {0}, s_ratio = 0, s_n = 0;
   double z_it[3] = {0}, z_rd[3] = {0}, z_ratio[3] = {0}, z_n[3] = {0};
   double g_c[2] = {0}, g_it[2] = {0}, g_rd[2] = {0}, d_c[2] = {0};
   double x_it[4] = {0, 0, 0, 0}, x_rounds[4] = {0, 0, 0, 0};
-  double a_plain_max = 0, b_plain = 0, c_maxins = 0, b_maxins = 0, d_it[2] = {0, 0}, d_rounds[2] = {0, 0}, d_ins[2] = {0, 0};
+  double a_plain_max = 0, b_plain = 0, c_maxins = 0, b_maxins = 0, d_it[3] = {0, 0, 0}, d_rounds[3] = {0, 0, 0}, d_ins[3] = {0, 0, 0};
   for (int s = 0; s < sample; s++) {
     const long t0 = waves[s] * 64;
     Packet W, Wp, Wc;
@@ -607,6 +684,7 @@ int main(int argc, char** argv) {
             const long c = (long)(t + 1) * (1L << lev) - 1 + j;
             if (c < N) d[m++] = dist2(q, &T[c]);
           }
+        if (getenv("ZONLY")) zc[l] = nextafterf(R2, 0.f);   // no leader bound: the subtree's alone
         if (m >= K) {
           qsort(d, m, sizeof(float), cmp_fl);
           const float b = d[K - 1] * (1.f + 1e-6f);
@@ -639,7 +717,7 @@ int main(int argc, char** argv) {
       x_it[f] += wave_lockstep(W.q, xc, 0, &rounds, &li);
       x_rounds[f] += rounds;
     }
-    for (int pol = 0; pol < 2; pol++) {
+    for (int pol = 0; pol < 3; pol++) {
       int rounds = 0;
       long li = 0;
       d_it[pol] += wave_lockstep(W.q, W.cut, pol, &rounds, &li);
@@ -707,15 +785,106 @@ int main(int argc, char** argv) {
          "points/lane %.1f (wave max %.1f), inserts/lane %.1f; VALU model wave max %.0f vs A %.0f\n",
          BUCKET, e_nodes / S / 64, e_max_nodes / S, e_buckets / S / 64, e_pts / S / 64, e_max_pts / S, e_ins / S / 64,
          e_max_cost / S, 55.0 * a_max / S);
-  for (int pol = 0; pol < 2; pol++)
+  for (int pol = 0; pol < 3; pol++)
     printf("D lockstep wave (QL %d, %s rounds): iterations %.1f, rounds %.1f, inserts/lane %.1f\n", QL,
-           pol ? "batch-merge" : "pop-one", d_it[pol] / S, d_rounds[pol] / S, d_ins[pol] / S / 64);
+           pol == 2 ? "filtered pop-one" : pol ? "batch-merge" : "pop-one", d_it[pol] / S, d_rounds[pol] / S,
+           d_ins[pol] / S / 64);
   for (int v = 0; v < 3; v++)
     printf("Z own subtree of %d nodes: cut/exact mean %.3f, iterations %.1f, rounds %.1f, VALU %.0f\n",
            (2 << (5 + v)) - 1, z_ratio[v] / z_n[v], z_it[v] / S, z_rd[v] / S, (z_it[v] * 60 + z_rd[v] * 111) / S);
   for (int v = 0; v < 2; v++)
     printf("G bucketed bottom (DB %d), %s cut: iterations %.1f, rounds %.1f, VALU %.0f vs current walk %.0f\n", DB,
            v ? "exact" : "seeded", g_it[v] / S, g_rd[v] / S, g_c[v] / S, d_c[v] / S);
+  if (getenv("LEADZ")) {   // leader waves (64 leaders, ranks 16 apart): plain cut vs own-subtree seeds
+    double it0 = 0, rd0 = 0, it1[3] = {0}, rd1[3] = {0};
+    srand(99);
+    const int LS = 100;
+    for (int s = 0; s < LS; s++) {
+      const long j0 = (long)((double)rand() / RAND_MAX * (nl - 70));
+      static const float* lq[64];
+      static float lc[64], zc[64];
+      for (int l = 0; l < 64; l++) { lq[l] = &Q[3 * ord[(j0 + l) * STRIDE]]; lc[l] = nextafterf(R2, 0.f); }
+      int rd = 0;
+      it0 += wave_lockstep(lq, lc, 0, &rd, &(long){0});
+      rd0 += rd;
+      for (int v = 0; v < 3; v++) {
+        const int h = 5 + v;
+        for (int l = 0; l < 64; l++) {
+          const float* q = lq[l];
+          zc[l] = nextafterf(R2, 0.f);
+          int t = 0, dep = 0;
+          while (dep < DB + 2 - h) {
+            const Node* nd = &T[t];
+            const float diff = q[nd->dim] - nd->p[nd->dim];
+            const int c = 2 * t + 1 + (diff > 0.f);
+            if (c >= N) break;
+            t = c; dep++;
+          }
+          static float d[1024];
+          int m = 0;
+          for (int lev = 0; lev <= h; lev++)
+            for (long j = 0; j < (1L << lev); j++) {
+              const long c = (long)(t + 1) * (1L << lev) - 1 + j;
+              if (c < N) d[m++] = dist2(q, &T[c]);
+            }
+          if (m >= K) {
+            qsort(d, m, sizeof(float), cmp_fl);
+            const float b = d[K - 1] * (1.f + 1e-6f);
+            if (b < zc[l]) zc[l] = b;
+          }
+        }
+        rd = 0;
+        it1[v] += wave_lockstep(lq, zc, 0, &rd, &(long){0});
+        rd1[v] += rd;
+      }
+    }
+    printf("L leader waves, plain cut: iterations %.1f, rounds %.1f\n", it0 / LS, rd0 / LS);
+    for (int v = 0; v < 3; v++)
+      printf("L leader waves, own-subtree (%d nodes) seed: iterations %.1f, rounds %.1f\n", (2 << (5 + v)) - 1,
+             it1[v] / LS, rd1[v] / LS);
+  }
+  if (getenv("POOL")) {   // P: pooled lanes over 4 waves' worth of consecutive followers
+    double pit[3] = {0}, prd[3] = {0};
+    const int refills[3] = {1, 8, 16};
+    srand(4242);
+    const int PS = 100;
+    for (int s = 0; s < PS; s++) {
+      const long t0 = (long)((double)rand() / RAND_MAX * (nwaves - 8)) * 64;
+      static const float* pq[256];
+      static float pc[256];
+      for (int i = 0; i < 256; i++) {
+        const long r = FRANK(t0 + i);
+        const float* q = &Q[3 * ord[r]];
+        float cut = nextafterf(R2, 0.f);
+        const long jp = r / STRIDE;
+        double b = 1e300;
+        for (long j = jp - 1; j <= jp + 2; j++)
+          if (j >= 0 && j < nl) {
+            if (lt[j] < -2.f) {   // leader not walked yet
+              walk_lane(&Q[3 * ord[j * STRIDE]], nextafterf(R2, 0.f), &L, &dummy);
+              lt[j] = L.n >= K ? key_d2(L.key[K - 1]) : -1.f;
+            }
+            b = fmin(b, seed_bound(&Q[3 * ord[j * STRIDE]], lt[j], q));
+          }
+        if (b < cut) cut = (float)b * (1.f + 1e-7f);
+        pq[i] = q; pc[i] = cut;
+      }
+      for (int v = 0; v < 3; v++) {
+        int rd = 0;
+        pit[v] += pool_lockstep(pq, pc, 256, refills[v], &rd);
+        prd[v] += rd;
+      }
+      // static: 4 waves of 64
+      for (int w = 0; w < 4; w++) {
+        int rd = 0;
+        pit_static += wave_lockstep(pq + 64 * w, pc + 64 * w, 0, &rd, &(long){0});
+        prd_static += rd;
+      }
+    }
+    printf("P static 4 waves x 64: iterations %.1f, rounds %.1f per 256 queries\n", pit_static / PS, prd_static / PS);
+    for (int v = 0; v < 3; v++)
+      printf("P pooled 256 queries, refill at %d idle: iterations %.1f, rounds %.1f\n", refills[v], pit[v] / PS, prd[v] / PS);
+  }
   printf("seeded (triangle) cut / exact k-th d2: mean %.3f\n", s_ratio / s_n);
   for (int v = 0; v < 8; v++)
     printf("Y %s leader list kk=%d: cut/exact mean %.3f, iterations %.1f, rounds %.1f\n", v >> 2 ? "two" : "nearest",
