@@ -424,6 +424,48 @@ __device__ __forceinline__ float follower_cut(const float4* __restrict__ lead, i
   return seed_cut(b, R2);
 }
 
+// Leader cut-off from the leader's own kd subtree. The six complete levels
+// under the depth-(D - 6) node on q's close path (D = the deepest, possibly
+// partial level) hold 63 photons, so their 50th-smallest d^2 -- the 14th
+// largest, kept in a descending v_med3 list -- bounds the K-th nearest d^2:
+// at least 50 photons lie within it. d^2 is computed exactly as the walk does,
+// so the bound admits them; it only prunes (results stay those of the plain
+// walk). Without it a leader whose neighbourhood is sparse walks under the
+// plain 100-unit radius until its list fills: on the Cornell box (config 2)
+// some leader walks ran tens of thousands of steps and the under-filled
+// leader launch (231k queries) took 16.8 ms.
+constexpr int kSubtreeLevels = 6;   // 63 nodes
+constexpr int kSubtreeTop = (1 << kSubtreeLevels) - 1 - (kKNearest - 1);   // 14: rank 50 of 63 from the top
+template <bool WIDE>
+__device__ __forceinline__ float subtree_cut(const float4* __restrict__ nodes, uint32_t n, v3 q, float plain) {
+  const int D = 31 - __clz(n);   // deepest level (0-based): levels 0 .. D - 1 are complete
+  const int dz = D - kSubtreeLevels;
+  if (dz < 0) return plain;
+  uint32_t c1 = 1;
+  for (int d = 0; d < dz; d++) {   // close path
+    const float4 nd = node1<WIDE>(nodes, c1);
+    const uint32_t dim = __float_as_uint(nd.w) & 3u;
+    const float diff = dim == 0 ? q.x - nd.x : (dim == 1 ? q.y - nd.y : q.z - nd.z);
+    c1 = 2 * c1 + (diff > 0.f ? 1u : 0u);
+  }
+  float top[kSubtreeTop];   // descending
+#pragma unroll
+  for (int j = 0; j < kSubtreeTop; j++) top[j] = -1.f;
+#pragma unroll
+  for (int l = 0; l < kSubtreeLevels; l++) {
+#pragma unroll 4
+    for (uint32_t k = 0; k < (1u << l); k++) {
+      const float4 nd = node1<WIDE>(nodes, (c1 << l) + k);
+      const float dx = q.x - nd.x, dy = q.y - nd.y, dz2 = q.z - nd.z;
+      const float d2 = dx * dx + dy * dy + dz2 * dz2;
+#pragma unroll
+      for (int j = kSubtreeTop - 1; j > 0; j--) top[j] = __builtin_amdgcn_fmed3f(top[j - 1], top[j], d2);
+      top[0] = fmaxf(top[0], d2);
+    }
+  }
+  return fminf(top[kSubtreeTop - 1], plain);
+}
+
 // One level of the seeded gather. LEADERS: walk ranks 0, S, 2S, ... with the
 // plain cut-off, recording (position, K-th d^2) in lead[r / S]; followers:
 // every other rank (thread t -> rank (t / (S-1)) * S + 1 + t % (S-1)), cut-off
@@ -442,7 +484,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   const v3 q = {qq.x, qq.y, qq.z};
   const float R2 = kKMaxDistance * kKMaxDistance;
-  const float cut = (valid && !LEADERS) ? follower_cut(lead, nq, r, q, R2) : lean_cut(R2);
+  float cut = lean_cut(R2);
+  if (valid) cut = LEADERS ? subtree_cut<WIDE>(nodes, (uint32_t)n, q, cut) : follower_cut(lead, nq, r, q, R2);
   double list[kKNearest];
   knn_walk_lean<kKNearest, kGatherQL, WIDE>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
   if (valid) {

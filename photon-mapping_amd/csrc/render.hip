@@ -458,12 +458,9 @@ static hipError_t sort_queries(const float4* dense, int64_t n, const pm_box& bb,
 static hipError_t gather_sorted(const pm_photon_map* m, SortedQueries& Q, float4* res, int tag, hipStream_t s,
                                 int k = kKNearest) {
   if (Q.n <= 0) return hipSuccess;
-  {
-    PhaseTimer tg(tag == 1 ? PH_GATHER_GLOBAL : PH_COUNT, s);
-    // lanes take the queries in Morton order and write each result in place
-    if (k == kKNearest) PM_HIP_TRY(launch_gather(m, Q.dense, Q.n, res, s, tag, Q.perm.p));
-    else PM_HIP_TRY(launch_gather_k(m, Q.dense, Q.n, res, s, k, Q.perm.p));
-  }
+  // lanes take the queries in Morton order and write each result in place
+  if (k == kKNearest) PM_HIP_TRY(launch_gather(m, Q.dense, Q.n, res, s, tag, Q.perm.p));
+  else PM_HIP_TRY(launch_gather_k(m, Q.dense, Q.n, res, s, k, Q.perm.p));
   return hipSuccess;
 }
 
@@ -561,6 +558,10 @@ struct pm_render_job {
   pm_render_stats stats{};
   pm_scene* scene = nullptr;
   bool finished = false;
+  hipStream_t side = nullptr;   // the caustic gather's stream (render_finish), created on first use
+  ~pm_render_job() {
+    if (side) (void)hipStreamDestroy(side);
+  }
 };
 
 namespace pmd {
@@ -732,9 +733,40 @@ hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_p
                          float* rgb, hipStream_t s) {
   if (J->nthreads == 0) return hipSuccess;
   {
+    // The two gathers are independent: the caustic one runs on a side stream
+    // beside the global one. The global map's leader launch (every 16th
+    // query) ends with its slowest waves while most of the GPU idles -- on the
+    // Cornell box (config 2) 231k leaders, fewer waves than the GPU holds, and
+    // a few leaders walk thousands of nodes -- and the caustic gather fills it.
+    // The global gather is enqueued first: a k != 50 caustic gather
+    // synchronises its own stream before it returns.
+    // (The global gather's own time comes from events read after the final
+    // synchronisation: a host wait between the two would serialise them.)
     PhaseTimer tm(PH_GATHER, s);
-    PM_HIP_TRY(gather_sorted(cmap, J->cs, J->cres.p, 0, s, J->A.caustic_k));
-    PM_HIP_TRY(gather_sorted(gmap, J->gs, J->gres.p, 1, s));
+    if (!J->side) PM_HIP_TRY(hipStreamCreateWithFlags(&J->side, hipStreamNonBlocking));
+    hipEvent_t ready = nullptr, done = nullptr, g0 = nullptr, g1 = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreate(&g0);
+    if (e == hipSuccess) e = hipEventCreate(&g1);
+    if (e == hipSuccess) e = hipEventRecord(ready, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(J->side, ready, 0);
+    if (e == hipSuccess) e = hipEventRecord(g0, s);
+    if (e == hipSuccess) e = gather_sorted(gmap, J->gs, J->gres.p, 1, s);
+    if (e == hipSuccess) e = hipEventRecord(g1, s);
+    if (e == hipSuccess) {
+      AllocStream side_pool(J->side);   // the side gather's temporaries belong to its stream
+      e = gather_sorted(cmap, J->cs, J->cres.p, 0, J->side, J->A.caustic_k);
+    }
+    if (e == hipSuccess) e = hipEventRecord(done, J->side);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, done, 0);
+    if (e == hipSuccess) e = hipEventSynchronize(g1);
+    float ms = 0.f;
+    if (e == hipSuccess && hipEventElapsedTime(&ms, g0, g1) == hipSuccess) record_phase_us(PH_GATHER_GLOBAL, ms * 1e3);
+    if (e != hipSuccess) (void)hipStreamSynchronize(J->side);   // no side work outlives a failed call
+    for (hipEvent_t ev : {ready, done, g0, g1})
+      if (ev) (void)hipEventDestroy(ev);
+    PM_HIP_TRY(e);
   }
   PathOut O{J->vdirect.p, J->vatt.p, J->valb.p, J->vflags.p, J->cq.p, J->cvalid.p, J->gq.p, J->galb.p,
             J->gvalid.p,  J->gdir.p, J->sray.p, J->sterm.p, J->svis.p, J->rays.p,  J->next.p, J->ovf.p,

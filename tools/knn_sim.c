@@ -68,6 +68,22 @@ static void build(int t, int* v, int s) {
   if (mx[1] - mn[1] > mx[dim] - mn[dim]) dim = 1;
   if (mx[2] - mn[2] > mx[dim] - mn[dim]) dim = 2;
   const int ls = left_size(s);
+  if (getenv("CLEAN") && s > 2) {
+    // tie-aware: the widest dimension whose median has no equal coordinate
+    // among its rank neighbours (ls - 1, ls + 1); else the widest
+    int best = -1;
+    for (int d = 0; d < 3; d++) {
+      cmp_dim = d;
+      select_k(v, s, ls);
+      const float m = P[3 * v[ls] + d];
+      float lo = -FLT_MAX, hi = FLT_MAX;
+      for (int i = 0; i < ls; i++) lo = fmaxf(lo, P[3 * v[i] + d]);
+      for (int i = ls + 1; i < s; i++) hi = fminf(hi, P[3 * v[i] + d]);
+      const int clean = lo < m && m < hi;
+      if (clean && (best < 0 || mx[d] - mn[d] > mx[best] - mn[best])) best = d;
+    }
+    if (best >= 0) dim = best;
+  }
   cmp_dim = dim;
   select_k(v, s, ls);
   const int e = v[ls];
@@ -158,6 +174,7 @@ static float kth_of_sets(const float* q, int** sets, const int* ns, int nsets) {
 }
 
 // ---- A: per-lane JUMP walk (lean_step), returns node loads; counts inserts
+static int VERBOSE = 0;
 static int walk_lane(const float* q, float cut, List* L, int* ins) {
   list_init(L);
   int prev = -1, curr = 0, depth = 0, steps = 0;
@@ -173,7 +190,11 @@ static int walk_lane(const float* q, float cut, List* L, int* ins) {
     const int test = (down && close >= N) || prev == close;
     if (test) {
       const float d2 = dist2(q, nd);
-      if (d2 <= cut && list_insert(L, mkkey(d2, nd->id))) { (*ins)++; bound = bound_of(L, cut); }
+      if (d2 <= cut && list_insert(L, mkkey(d2, nd->id))) {
+        (*ins)++;
+        bound = bound_of(L, cut);
+        if (VERBOSE && (*ins <= 60 || *ins % 20 == 0)) printf("      step %d depth %d insert #%d d2 %g bound %g node (%g %g %g)\n", steps, depth, *ins, d2, bound, nd->p[0], nd->p[1], nd->p[2]);
+      }
     }
     int next, nprev;
     if (down && close < N) {
@@ -795,6 +816,114 @@ int main(int argc, char** argv) {
   for (int v = 0; v < 2; v++)
     printf("G bucketed bottom (DB %d), %s cut: iterations %.1f, rounds %.1f, VALU %.0f vs current walk %.0f\n", DB,
            v ? "exact" : "seeded", g_it[v] / S, g_rd[v] / S, g_c[v] / S, d_c[v] / S);
+  if (getenv("LEADALL")) {   // every leader wave with the plain cut: worst waves
+    const long nw = nl / 64;
+    int worst[5] = {0}; long wj[5] = {0};
+    double tot = 0;
+    for (long wv = 0; wv < nw; wv++) {
+      static const float* lq[64];
+      static float lc[64];
+      for (int l = 0; l < 64; l++) { lq[l] = &Q[3 * ord[(wv * 64 + l) * STRIDE]]; lc[l] = nextafterf(R2, 0.f); }
+      int rd = 0;
+      const int it = wave_lockstep(lq, lc, 0, &rd, &(long){0});
+      tot += it;
+      for (int k = 0; k < 5; k++) if (it > worst[k]) { for (int m = 4; m > k; m--) { worst[m] = worst[m-1]; wj[m] = wj[m-1]; } worst[k] = it; wj[k] = wv; break; }
+    }
+    // R: close-path seed with retry: cut0 = F x max d2 of the last 6 close-path nodes;
+    // a lane whose list does not fill walks again with the plain cut
+    for (int fv = 0; fv < 3; fv++) {
+      const float F = fv == 0 ? 4.f : (fv == 1 ? 16.f : 64.f);
+      double rt = 0, rmax = 0, fails = 0;
+      long rw[3] = {0};
+      for (long wv = 0; wv < nw; wv++) {
+        double wmax = 0;
+        for (int l = 0; l < 64; l++) {
+          const float* q = &Q[3 * ord[(wv * 64 + l) * STRIDE]];
+          int t = 0, dep = 0;
+          float last[64];
+          int nl2 = 0;
+          while (t < N) {
+            const Node* nd = &T[t];
+            last[nl2++] = dist2(q, nd);
+            const float diff = q[nd->dim] - nd->p[nd->dim];
+            t = 2 * t + 1 + (diff > 0.f);
+            dep++;
+          }
+          float mx = 0.f;
+          for (int i = nl2 - 6 < 0 ? 0 : nl2 - 6; i < nl2; i++) mx = fmaxf(mx, last[i]);
+          const float c0 = fminf(mx * F, nextafterf(R2, 0.f));
+          int ins = 0;
+          double cost = dep + walk_lane(q, c0, &L, &ins);
+          if (L.n < K && c0 < nextafterf(R2, 0.f)) { cost += walk_lane(q, nextafterf(R2, 0.f), &L, &ins); fails++; }
+          rt += cost;
+          if (cost > wmax) wmax = cost;
+        }
+        rmax += wmax;
+        if (wmax > rw[0]) rw[0] = (long)wmax;
+      }
+      printf("R close-path seed x%g + retry: mean lane steps %.1f, mean wave max %.1f, worst wave %ld, lanes retried %.3f%%\n", F,
+             rt / nw / 64, rmax / nw, rw[0], fails / nw / 64 * 100);
+    }
+    {
+      double pt = 0, pmax = 0, pw = 0;
+      for (long wv = 0; wv < nw; wv++) {
+        double wmax = 0;
+        for (int l = 0; l < 64; l++) {
+          int ins = 0;
+          const double c = walk_lane(&Q[3 * ord[(wv * 64 + l) * STRIDE]], nextafterf(R2, 0.f), &L, &ins);
+          pt += c;
+          if (c > wmax) wmax = c;
+        }
+        pmax += wmax;
+        if (wmax > pw) pw = wmax;
+      }
+      printf("R plain cut: mean lane steps %.1f, mean wave max %.1f, worst wave %.0f\n", pt / nw / 64, pmax / nw, pw);
+    }
+    printf("LA all %ld leader waves: mean iterations %.1f, worst %d %d %d %d %d (waves %ld %ld ...)\n", nw, tot / nw,
+           worst[0], worst[1], worst[2], worst[3], worst[4], wj[0], wj[1]);
+    // the worst wave's lanes
+    {
+      const long wv = wj[0];
+      for (int l = 0; l < 64; l++) {
+        const float* q = &Q[3 * ord[(wv * 64 + l) * STRIDE]];
+        int ins = 0;
+        const int st = walk_lane(q, nextafterf(R2, 0.f), &L, &ins);
+        if (st > 2000) {
+          printf("  lane %d q (%g %g %g) steps %d inserts %d kth d2 %g\n", l, q[0], q[1], q[2], st, ins,
+                 L.n >= K ? key_d2(L.key[K - 1]) : -1.f);
+          VERBOSE = 1;
+          { int ii = 0; const float vc = getenv("VCUT") ? (float)atof(getenv("VCUT")) : nextafterf(R2, 0.f);
+            const int st2 = walk_lane(q, vc, &L, &ii); printf("    verbose walk with cut %g: steps %d\n", vc, st2); }
+          VERBOSE = 0;
+          // replay: nodes entered as FAR children, by split dim and |diff|
+          static long hist[3][4];
+          memset(hist, 0, sizeof hist);
+          const float b = L.n >= K ? key_d2(L.key[K - 1]) : R2;
+          // exact-bound recursive search counting visits
+          long visits = 0;
+          int stk[256], sp = 0;
+          stk[sp++] = 0;
+          while (sp) {
+            const int t = stk[--sp];
+            if (t >= N) continue;
+            visits++;
+            const Node* nd = &T[t];
+            const float diff = q[nd->dim] - nd->p[nd->dim];
+            const int close = 2 * t + 1 + (diff > 0.f), far = 2 * t + 2 - (diff > 0.f);
+            if (far < N && diff * diff <= b) {
+              stk[sp++] = far;
+              hist[nd->dim][diff == 0.f ? 0 : (diff * diff < 1e-8f ? 1 : (diff * diff < b * 0.25f ? 2 : 3))]++;
+            }
+            stk[sp++] = close;
+          }
+          printf("    exact-bound visits %ld; far entries by dim [diff==0, tiny, <r/2, rest]: x %ld %ld %ld %ld y %ld %ld %ld %ld z %ld %ld %ld %ld\n",
+                 visits, hist[0][0], hist[0][1], hist[0][2], hist[0][3], hist[1][0], hist[1][1], hist[1][2], hist[1][3],
+                 hist[2][0], hist[2][1], hist[2][2], hist[2][3]);
+          break;
+        }
+      }
+    }
+  }
   if (getenv("LEADZ")) {   // leader waves (64 leaders, ranks 16 apart): plain cut vs own-subtree seeds
     double it0 = 0, rd0 = 0, it1[3] = {0}, rd1[3] = {0};
     srand(99);
