@@ -42,7 +42,7 @@ hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light*
                         hipStream_t s);
 hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba,
                          float* rgb, hipStream_t s);
-pm_render_job* render_job_new(pm_scene* sc);
+pm_render_job* render_job_new(pm_scene* sc, hipStream_t s);
 void render_job_delete(pm_render_job* J);
 const pm_render_stats& render_job_stats(const pm_render_job* J);
 pm_scene* render_job_scene(const pm_render_job* J);
@@ -644,7 +644,7 @@ int pm_render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lig
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
   reset_phase(PH_PATHS);
-  pm_render_job* J = render_job_new(sc);
+  pm_render_job* J = render_job_new(sc, s);
   if (!J) return PM_ERR_OOM;
   hipError_t e = render_begin(sc, P, lights, nl, J, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -559,6 +559,7 @@ struct pm_render_job {
   pm_scene* scene = nullptr;
   bool finished = false;
   hipStream_t side = nullptr;   // the caustic gather's stream (render_finish), created on first use
+  hipStream_t begun_on = nullptr;   // render_begin's stream: the job's buffers return to its allocator pool
   ~pm_render_job() {
     if (side) (void)hipStreamDestroy(side);
   }
@@ -566,12 +567,23 @@ struct pm_render_job {
 
 namespace pmd {
 
-pm_render_job* render_job_new(pm_scene* sc) {
+pm_render_job* render_job_new(pm_scene* sc, hipStream_t s) {
   pm_render_job* J = new (std::nothrow) pm_render_job();
-  if (J) J->scene = sc;
+  if (J) {
+    J->scene = sc;
+    J->begun_on = s;
+  }
   return J;
 }
-void render_job_delete(pm_render_job* J) { delete J; }
+// The job's buffers go back to the pool of the stream they were taken from:
+// freed under the destroying thread's stream (none outside an entry point),
+// a caller that begins every frame's job on a side stream would never get them
+// back there (each begin a fresh hipMalloc, until memory runs out).
+void render_job_delete(pm_render_job* J) {
+  if (!J) return;
+  AllocStream pool(J->begun_on);
+  delete J;
+}
 const pm_render_stats& render_job_stats(const pm_render_job* J) { return J->stats; }
 pm_scene* render_job_scene(const pm_render_job* J) { return J->scene; }
 bool render_job_finished(const pm_render_job* J) { return J->finished; }

@@ -46,6 +46,11 @@ class FrameConfig:
     shard_build: bool = True
     # neighbours of the caustic gather (0: the reference's 50; config 5: 200)
     caustic_k: int = 0
+    # run pm_render_begin (map-independent: camera paths, shadow and final-gather
+    # rays, direct light, sorted queries) on a side stream from a second host
+    # thread while the photons are traced and the maps built; it fills the
+    # kd build's small, under-filled launches (config 3: ~0.6 ms per frame)
+    overlap_render: bool = True
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -279,6 +284,49 @@ class GpuBackend:
         self.phase["kdbuild"] = self.phase.get("kdbuild", 0.0) + kd
         return gm
 
+    def start_render(self, tile_rank: int, tile_count: int):
+        """pm_render_begin on a side stream from a second host thread; returns a
+        handle for finish_render. The begin half synchronises its stream before
+        it returns, so the job is complete once the thread has ended."""
+        import threading
+        import torch
+        pm, c = self.pm, self.cfg
+        if getattr(self, "_rside", None) is None:
+            self._rside = torch.cuda.Stream()
+        side, box = self._rside, {}
+
+        def run():
+            try:
+                job = pm.render_begin(self.scene, self.cam, c.width, c.height, c.spp, c.depth, c.sky, self.lights,
+                                      tile_rank=tile_rank, tile_count=tile_count, stream=side.cuda_stream,
+                                      caustic_k=c.caustic_k)
+                box["r"] = (job, pm.phase_us("paths"))   # phase timers are per host thread
+            except BaseException as e:   # re-raised by finish_render / join_render
+                box["e"] = e
+
+        th = threading.Thread(target=run, name="pm-render-begin")
+        th.start()
+        return th, box
+
+    @staticmethod
+    def join_render(pending):
+        th, box = pending
+        th.join()
+        if "e" in box:
+            raise box["e"]
+        return box["r"]
+
+    def finish_render(self, pending, gm, cm, rgba):
+        job, paths_us = self.join_render(pending)
+        try:
+            job.finish(gm, cm, want_rgb=False, rgba=rgba)
+        finally:
+            job.close()
+        self.phase["paths"] = paths_us
+        for k in ("gather", "gather_global", "resolve"):
+            self.phase[k] = self.pm.phase_us(k)
+        return rgba
+
     def render(self, gm, cm, tile_rank: int, tile_count: int, rgba):
         pm = self.pm
         c = self.cfg
@@ -291,10 +339,40 @@ class GpuBackend:
 
 def frame(backend, rank: int, world: int, dist=None, rgba=None):
     """One frame through `backend`; returns (rgba on rank 0 (merged), info).
-    N > 1: the caustic photons are exchanged first (small), then the global
-    photons' all-gather runs on RCCL's stream while the caustic map is built;
-    phases_us["exchange"] is that window (HIP events), caustic build included."""
+    With cfg.overlap_render (backends that have start_render), the render's
+    map-independent half runs on a side stream beside the trace and the map
+    builds; the phases then add up to more than the frame. N > 1: the caustic
+    photons are exchanged first (small), then the global photons' all-gather
+    runs on RCCL's stream while the caustic map is built; phases_us["exchange"]
+    is that window (HIP events), caustic build included."""
     backend.phase = {}
+    pending = None
+    if backend.cfg.overlap_render and hasattr(backend, "start_render"):
+        pending = backend.start_render(rank, world)
+    try:
+        g, c, gm, cm = _maps(backend, rank, world, dist)
+    except BaseException:
+        if pending is not None:   # no side work outlives a failed frame
+            try:
+                backend.join_render(pending)[0].close()
+            except BaseException:
+                pass
+        raise
+    if world > 1 and rgba is not None:
+        rgba.zero_()   # tiles are disjoint: the SUM-reduce needs zeros outside this rank's tiles
+    if pending is not None:
+        rgba = backend.finish_render(pending, gm, cm, rgba)
+    else:
+        rgba = backend.render(gm, cm, rank, world, rgba)
+    if world > 1:
+        dist.reduce(rgba, dst=0, op=dist.ReduceOp.SUM)
+    info = {"n_global": int(gm.n), "n_caustic": int(cm.n), "n_global_rows": int(g.shape[0]),
+            "us": dict(backend.phase)}
+    return rgba, info
+
+
+def _maps(backend, rank: int, world: int, dist):
+    """Trace both photon sets, exchange them (N > 1), build both maps."""
     g = backend.trace(False, rank, world)
     c = backend.trace(True, rank, world)
     if backend.cfg.quantize:   # elementwise: the same before or after the exchange
@@ -312,11 +390,4 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
         backend.phase["exchange"] = 0.0
         cm = backend.caustic_map(c)
     gm = backend.global_map(g, c, rank, world, dist)
-    if world > 1 and rgba is not None:
-        rgba.zero_()   # tiles are disjoint: the SUM-reduce needs zeros outside this rank's tiles
-    rgba = backend.render(gm, cm, rank, world, rgba)
-    if world > 1:
-        dist.reduce(rgba, dst=0, op=dist.ReduceOp.SUM)
-    info = {"n_global": int(gm.n), "n_caustic": int(cm.n), "n_global_rows": int(g.shape[0]),
-            "us": dict(backend.phase)}
-    return rgba, info
+    return g, c, gm, cm
