@@ -37,11 +37,15 @@ __device__ __forceinline__ int left_size(int s) {
 
 __device__ __forceinline__ float coord_of(const float4 e, int d) { return d == 0 ? e.x : (d == 1 ? e.y : e.z); }
 
-__global__ void k_kd_init_keys(const float4* elems, int64_t n, int d, uint32_t* keys, uint32_t* vals) {
+// orderable keys of the three coordinates in one pass over the elements
+__global__ void k_kd_init_keys(const float4* __restrict__ elems, int64_t n, uint32_t* __restrict__ kx,
+                               uint32_t* __restrict__ ky, uint32_t* __restrict__ kz) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  keys[i] = orderable_key(coord_of(elems[i], d));
-  vals[i] = (uint32_t)i;
+  const float4 e = elems[i];
+  kx[i] = orderable_key(e.x);
+  ky[i] = orderable_key(e.y);
+  kz[i] = orderable_key(e.z);
 }
 
 // The presorted lists: list d (sorted on dimension d) in buffer k (0 / 1) as
@@ -51,17 +55,6 @@ struct KdLists {
   int64_t n;
   __host__ __device__ float* comp(int d, int k, int c) const { return base + (int64_t)((d * 2 + k) * 4 + c) * n; }
 };
-
-__global__ void k_kd_gather_soa(const float4* __restrict__ elems, const uint32_t* __restrict__ order, int64_t n,
-                                KdLists Lst, int d) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float4 e = elems[order[i]];
-  Lst.comp(d, 0, 0)[i] = e.x;
-  Lst.comp(d, 0, 1)[i] = e.y;
-  Lst.comp(d, 0, 2)[i] = e.z;
-  Lst.comp(d, 0, 3)[i] = e.w;
-}
 
 __device__ __forceinline__ float4 kd_elem(const KdLists& Lst, int d, int k, int64_t p) {
   return make_float4(Lst.comp(d, k, 0)[p], Lst.comp(d, k, 1)[p], Lst.comp(d, k, 2)[p], Lst.comp(d, k, 3)[p]);
@@ -757,14 +750,16 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
   if (!lists.p) return hipErrorOutOfMemory;
   const KdLists Lst{lists.p, n};
   {
-    DevBuf<uint32_t> keys(n), vals(n);
-    if (!keys.p || !vals.p) return hipErrorOutOfMemory;
+    // presort: list d = the elements stably sorted on (orderable coordinate d,
+    // index); keys of all three coordinates in one pass, the index implicit in
+    // the first radix pass and the gather of the elements fused into the last
+    DevBuf<uint32_t> keys((size_t)3 * n);
+    if (!keys.p) return hipErrorOutOfMemory;
+    k_kd_init_keys<<<grid_for(n, 256), 256, 0, s>>>(elems, n, keys.p, keys.p + n, keys.p + 2 * n);
+    PM_HIP_TRY(hipGetLastError());
     for (int d = 0; d < 3; d++) {
-      k_kd_init_keys<<<grid_for(n, 256), 256, 0, s>>>(elems, n, d, keys.p, vals.p);
-      PM_HIP_TRY(hipGetLastError());
-      PM_HIP_TRY(radix_sort_pairs(keys.p, vals.p, n, 32, s));
-      k_kd_gather_soa<<<grid_for(n, 256), 256, 0, s>>>(elems, vals.p, n, Lst, d);
-      PM_HIP_TRY(hipGetLastError());
+      const SoaOut out{{Lst.comp(d, 0, 0), Lst.comp(d, 0, 1), Lst.comp(d, 0, 2), Lst.comp(d, 0, 3)}};
+      PM_HIP_TRY(radix_sort_gather_soa(keys.p + (int64_t)d * n, n, elems, out, s));
     }
   }
   DevBuf<int32_t> tb(cap), ts(cap), tls(cap), tdim(cap), tid(cap), tsel(cap);

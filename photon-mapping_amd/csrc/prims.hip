@@ -223,11 +223,17 @@ __global__ __launch_bounds__(kSortBlock) void k_sort_hist(const uint32_t* keys, 
 // stable), then the tile is ranked into LDS in digit order and written out so
 // that consecutive threads store consecutive positions of each digit's run.
 // (Loading inside 16 barrier-separated rounds left the pass latency-bound.)
+// IOTA: the values are the input positions (not read: the first pass of a sort
+// by index). ELEMS != nullptr (the last pass of the kd presort): no keys or
+// values are written; each sorted position receives elems[value] as four SoA
+// arrays (the gather by sorted index fused into the write-out).
+template <bool IOTA, bool SOA>
 __global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const uint32_t* __restrict__ keys,
                                                              const uint32_t* __restrict__ vals,
                                                              uint32_t* __restrict__ okeys, uint32_t* __restrict__ ovals,
                                                              int64_t n, int shift, const uint32_t* __restrict__ hist,
-                                                             const uint32_t* __restrict__ hoff, int nblocks) {
+                                                             const uint32_t* __restrict__ hoff, int nblocks,
+                                                             const float4* __restrict__ elems, SoaOut soa) {
   __shared__ uint32_t lkey[kSortTile], lval[kSortTile];
   __shared__ uint32_t lstart[256], gbase[256];
   __shared__ uint32_t wcnt[kSortBlock / 64][256];
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const uint32_t* __r
   for (int r = 0; r < kSub; r++) {
     const int64_t i = wbase + r * 64 + lane;
     kr[r] = i < n ? keys[i] : 0u;
-    vr[r] = i < n ? vals[i] : 0u;
+    vr[r] = IOTA ? (uint32_t)i : (i < n ? vals[i] : 0u);
   }
   // local digit starts = exclusive scan of this tile's histogram
   const uint32_t c = hist[(int64_t)tid * nblocks + blockIdx.x];
@@ -303,8 +309,16 @@ __global__ __launch_bounds__(kSortBlock) void k_sort_scatter(const uint32_t* __r
     const uint32_t key = lkey[p];
     const uint32_t dg = (key >> shift) & 0xFF;
     const uint32_t o = gbase[dg] + (uint32_t)p - lstart[dg];
-    okeys[o] = key;
-    ovals[o] = lval[p];
+    if (SOA) {
+      const float4 e = elems[lval[p]];
+      soa.c[0][o] = e.x;
+      soa.c[1][o] = e.y;
+      soa.c[2][o] = e.z;
+      soa.c[3][o] = e.w;
+    } else {
+      okeys[o] = key;
+      ovals[o] = lval[p];
+    }
   }
 }
 
@@ -319,7 +333,8 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, int64_t n, int end_b
     k_sort_hist<<<nb, kSortBlock, 0, s>>>(ka, n, shift, hist.p, nb);
     PM_HIP_TRY(hipGetLastError());
     PM_HIP_TRY(exclusive_scan_u32(hist.p, hoff.p, (int64_t)256 * nb, nullptr, s));
-    k_sort_scatter<<<nb, kSortBlock, 0, s>>>(ka, va, kb, vb, n, shift, hist.p, hoff.p, nb);
+    k_sort_scatter<false, false><<<nb, kSortBlock, 0, s>>>(ka, va, kb, vb, n, shift, hist.p, hoff.p, nb, nullptr,
+                                                            SoaOut{});
     PM_HIP_TRY(hipGetLastError());
     uint32_t* t = ka; ka = kb; kb = t;
     t = va; va = vb; vb = t;
@@ -327,6 +342,38 @@ hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, int64_t n, int end_b
   if (passes & 1) {
     PM_HIP_TRY(hipMemcpyAsync(keys, ka, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     PM_HIP_TRY(hipMemcpyAsync(vals, va, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  }
+  return hipSuccess;
+}
+
+hipError_t radix_sort_gather_soa(const uint32_t* keys, int64_t n, const float4* elems, const SoaOut& out,
+                                 hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int nb = (int)((n + kSortTile - 1) / kSortTile);
+  DevBuf<uint32_t> ka(n), kb(n), va(n), vb(n), hist((size_t)256 * nb), hoff((size_t)256 * nb);
+  if (!ka.p || !kb.p || !va.p || !vb.p || !hist.p || !hoff.p) return hipErrorOutOfMemory;
+  const uint32_t* kin = keys;
+  const uint32_t* vin = nullptr;
+  uint32_t *ko = ka.p, *vo = va.p;
+  for (int pass = 0; pass < 4; pass++) {
+    const int shift = 8 * pass;
+    k_sort_hist<<<nb, kSortBlock, 0, s>>>(kin, n, shift, hist.p, nb);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(exclusive_scan_u32(hist.p, hoff.p, (int64_t)256 * nb, nullptr, s));
+    if (pass == 0)
+      k_sort_scatter<true, false><<<nb, kSortBlock, 0, s>>>(kin, nullptr, ko, vo, n, shift, hist.p, hoff.p, nb,
+                                                            nullptr, SoaOut{});
+    else if (pass < 3)
+      k_sort_scatter<false, false><<<nb, kSortBlock, 0, s>>>(kin, vin, ko, vo, n, shift, hist.p, hoff.p, nb,
+                                                             nullptr, SoaOut{});
+    else
+      k_sort_scatter<false, true><<<nb, kSortBlock, 0, s>>>(kin, vin, nullptr, nullptr, n, shift, hist.p, hoff.p,
+                                                            nb, elems, out);
+    PM_HIP_TRY(hipGetLastError());
+    kin = ko;
+    vin = vo;
+    ko = ko == ka.p ? kb.p : ka.p;
+    vo = vo == va.p ? vb.p : va.p;
   }
   return hipSuccess;
 }

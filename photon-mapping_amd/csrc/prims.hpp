@@ -52,6 +52,14 @@ hipError_t exclusive_scan_u64(const uint64_t* in, uint64_t* out, int64_t n, uint
 
 // Stable LSD radix sort on key bits [0, end_bit). Sorted data ends in keys/vals.
 hipError_t radix_sort_pairs(uint32_t* keys, uint32_t* vals, int64_t n, int end_bit, hipStream_t s);
+// The kd presort: stable sort of positions 0..n-1 by 32-bit keys (read-only),
+// writing elems[i] of the sorted positions as four SoA arrays (x, y, z, w). The
+// first pass takes the positions implicitly, the last one gathers the elements.
+struct SoaOut {
+  float* c[4];
+};
+hipError_t radix_sort_gather_soa(const uint32_t* keys, int64_t n, const float4* elems, const SoaOut& out,
+                                 hipStream_t s);
 
 // float -> uint32 whose unsigned order == float order, with -0 == +0.
 __host__ __device__ inline uint32_t orderable_key(float f) {

@@ -175,11 +175,17 @@ static float kth_of_sets(const float* q, int** sets, const int* ns, int nsets) {
 
 // ---- A: per-lane JUMP walk (lean_step), returns node loads; counts inserts
 static int VERBOSE = 0;
+static int BOXD = 0;   // incremental box-distance pruning (Arya-Mount) in the walk
 static int walk_lane(const float* q, float cut, List* L, int* ins) {
   list_init(L);
   int prev = -1, curr = 0, depth = 0, steps = 0;
   uint32_t far_mask = 0;
   float bound = cut;
+  float off[3] = {0.f, 0.f, 0.f}, rd = 0.f;
+  int odep[3] = {0, 0, 0};   // BOXD 3: depth of the far entry that set off[d]
+  int sdim[64];
+  float soff[64];
+  int sp = 0;
   for (;;) {
     const Node* nd = &T[curr];
     steps++;
@@ -199,8 +205,14 @@ static int walk_lane(const float* q, float cut, List* L, int* ins) {
     int next, nprev;
     if (down && close < N) {
       next = close; nprev = curr; far_mask &= ~(2u << depth); depth++;
-    } else if (far < N && diff * diff <= bound) {
+    } else if (far < N && (BOXD ? rd - off[nd->dim] * off[nd->dim] + diff * diff : diff * diff) <= bound) {
       next = far; nprev = curr; far_mask |= 2u << depth; depth++;
+      if (BOXD) {
+        rd = rd - off[nd->dim] * off[nd->dim] + diff * diff;
+        if (BOXD == 1) { sdim[sp] = nd->dim; soff[sp] = off[nd->dim]; sp++; }
+        off[nd->dim] = fabsf(diff);
+        odep[nd->dim] = depth;   // depth of the far child just entered
+      }
     } else {
       const uint32_t open = (~far_mask & ((2u << depth) - 1u)) | 1u;
       int da = 31;
@@ -208,6 +220,16 @@ static int walk_lane(const float* q, float cut, List* L, int* ins) {
       const int a = ((curr + 1) >> (depth - da)) - 1;
       next = da == 0 ? -1 : ((a + 1) >> 1) - 1;
       nprev = a;
+      if (BOXD == 1)
+        for (int u = 0; u < depth - da; u++) {   // unwind the far entries below a's parent
+          sp--;
+          off[sdim[sp]] = soff[sp];
+        }
+      if (BOXD == 2) off[0] = off[1] = off[2] = 0.f;   // conservative: forget every offset
+      if (BOXD == 3)                                    // forget the offsets set at or below a
+        for (int d = 0; d < 3; d++)
+          if (odep[d] >= da) off[d] = 0.f;
+      if (BOXD) rd = off[0] * off[0] + off[1] * off[1] + off[2] * off[2];
       depth = da - 1;
     }
     if (next < 0) break;
@@ -816,6 +838,51 @@ int main(int argc, char** argv) {
   for (int v = 0; v < 2; v++)
     printf("G bucketed bottom (DB %d), %s cut: iterations %.1f, rounds %.1f, VALU %.0f vs current walk %.0f\n", DB,
            v ? "exact" : "seeded", g_it[v] / S, g_rd[v] / S, g_c[v] / S, d_c[v] / S);
+  if (getenv("BOXCMP")) {   // per-lane steps, plain vs box-distance pruning, seeded followers + leaders
+    double sa[4] = {0}, mx[4] = {0}, ls[4] = {0}, lw[4] = {0};
+    for (int b = 0; b < 4; b++) {
+      BOXD = b;
+      srand(555);
+      for (int s2 = 0; s2 < 200; s2++) {
+        const long t0 = (long)((double)rand() / RAND_MAX * (nwaves - 2)) * 64;
+        double wm = 0;
+        for (int l = 0; l < 64; l++) {
+          const long r = FRANK(t0 + l);
+          const float* q = &Q[3 * ord[r]];
+          const long jp = r / STRIDE;
+          double bb = 1e300;
+          for (long j = jp - 1; j <= jp + 2; j++)
+            if (j >= 0 && j < nl) {
+              if (lt[j] < -2.f) { BOXD = 0; walk_lane(&Q[3 * ord[j * STRIDE]], nextafterf(R2, 0.f), &L, &dummy); BOXD = b;
+                                  lt[j] = L.n >= K ? key_d2(L.key[K - 1]) : -1.f; }
+              bb = fmin(bb, seed_bound(&Q[3 * ord[j * STRIDE]], lt[j], q));
+            }
+          const float cut = bb < R2 ? (float)bb * (1.f + 1e-7f) : nextafterf(R2, 0.f);
+          int ins = 0;
+          const int st = walk_lane(q, cut, &L, &ins);
+          sa[b] += st;
+          if (st > wm) wm = st;
+        }
+        mx[b] += wm;
+      }
+      const long nw2 = nl / 64;
+      for (long wv = 0; wv < nw2; wv++) {
+        double wm = 0;
+        for (int l = 0; l < 64; l++) {
+          int ins = 0;
+          const int st = walk_lane(&Q[3 * ord[(wv * 64 + l) * STRIDE]], nextafterf(R2, 0.f), &L, &ins);
+          ls[b] += st;
+          if (st > wm) wm = st;
+        }
+        if (wm > lw[b]) lw[b] = wm;
+      }
+      ls[b] /= nw2 * 64;
+    }
+    BOXD = 0;
+    for (int b = 0; b < 4; b++)
+      printf("BOX%d followers: mean lane steps %.1f, mean wave max %.1f; leaders: mean %.1f, worst %.0f\n", b,
+             sa[b] / 200 / 64, mx[b] / 200, ls[b], lw[b]);
+  }
   if (getenv("LEADALL")) {   // every leader wave with the plain cut: worst waves
     const long nw = nl / 64;
     int worst[5] = {0}; long wj[5] = {0};
