@@ -81,10 +81,12 @@ __global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TPOOL_WAVES) void k_ph_tr
       [&](int64_t i, const Ray&, const HitInfo& h) { hits[i] = make_float2(h.t, __int_as_float(h.slot)); });
 }
 
-// Surviving rays are appended with ONE atomic per 1024-thread block (a
-// same-address atomic per wave serialised at one L2 channel: ~2/3 of the
-// kernel).
-constexpr int kShadeBlock = 1024;
+// Surviving rays are appended with ONE atomic per block (a same-address atomic
+// per wave serialised at one L2 channel: ~2/3 of the kernel).
+#ifndef PM_SHADE_BLOCK
+#define PM_SHADE_BLOCK 256
+#endif
+constexpr int kShadeBlock = PM_SHADE_BLOCK;
 
 __global__ __launch_bounds__(kShadeBlock) void k_ph_shade(DevScene S, const PhotonRay* __restrict__ in,
                                                           const uint32_t* __restrict__ live,

@@ -284,10 +284,14 @@ class GpuBackend:
         self.phase["kdbuild"] = self.phase.get("kdbuild", 0.0) + kd
         return gm
 
-    def start_render(self, tile_rank: int, tile_count: int):
+    def start_render(self, tile_rank: int, tile_count: int, caustic_shard=None):
         """pm_render_begin on a side stream from a second host thread; returns a
         handle for finish_render. The begin half synchronises its stream before
-        it returns, so the job is complete once the thread has ended."""
+        it returns, so the job is complete once the thread has ended. With
+        caustic_shard=(rank, world) the same thread then traces the caustic
+        photons on that stream (take them with caustic_photons): its short,
+        latency-bound bounce launches fill the GPU beside the global trace's
+        tail instead of running after it."""
         import threading
         import torch
         pm, c = self.pm, self.cfg
@@ -301,12 +305,25 @@ class GpuBackend:
                                       tile_rank=tile_rank, tile_count=tile_count, stream=side.cuda_stream,
                                       caustic_k=c.caustic_k)
                 box["r"] = (job, pm.phase_us("paths"))   # phase timers are per host thread
+                if caustic_shard is not None:
+                    t = pm.run_point_light_ray_gen(self.scene, self.lights, c.caustic, c.max_depth, True,
+                                                   shard_rank=caustic_shard[0], shard_count=caustic_shard[1],
+                                                   out=self.cbuf, stream=side.cuda_stream)
+                    box["c"] = (t, pm.phase_us("trace") + pm.phase_us("compact"))
             except BaseException as e:   # re-raised by finish_render / join_render
                 box["e"] = e
 
         th = threading.Thread(target=run, name="pm-render-begin")
         th.start()
         return th, box
+
+    def caustic_photons(self, pending):
+        """The caustic photons traced by start_render(caustic_shard=...)'s thread
+        (complete: the thread synchronised its stream)."""
+        self.join_render(pending)
+        t, us = pending[1]["c"]
+        self.phase["trace"] = self.phase.get("trace", 0.0) + us
+        return t
 
     @staticmethod
     def join_render(pending):
@@ -348,9 +365,9 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     backend.phase = {}
     pending = None
     if backend.cfg.overlap_render and hasattr(backend, "start_render"):
-        pending = backend.start_render(rank, world)
+        pending = backend.start_render(rank, world, caustic_shard=(rank, world))
     try:
-        g, c, gm, cm = _maps(backend, rank, world, dist)
+        g, c, gm, cm = _maps(backend, rank, world, dist, pending)
     except BaseException:
         if pending is not None:   # no side work outlives a failed frame
             try:
@@ -371,10 +388,12 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     return rgba, info
 
 
-def _maps(backend, rank: int, world: int, dist):
-    """Trace both photon sets, exchange them (N > 1), build both maps."""
+def _maps(backend, rank: int, world: int, dist, pending=None):
+    """Trace both photon sets, exchange them (N > 1), build both maps. With a
+    render pending from start_render(caustic_shard=...), the caustic photons
+    come from its thread."""
     g = backend.trace(False, rank, world)
-    c = backend.trace(True, rank, world)
+    c = backend.caustic_photons(pending) if pending is not None else backend.trace(True, rank, world)
     if backend.cfg.quantize:   # elementwise: the same before or after the exchange
         g, c = backend.quantize(g), backend.quantize(c)
     if world > 1:
