@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--depth", type=int, default=30)
     ap.add_argument("--scene", default=None, choices=["sponza", "cornell"],
                     help="config 2: cornell, 3/5: sponza")
+    ap.add_argument("--frame-opt", action="append", default=[], metavar="FIELD=0|1",
+                    help="override a boolean pm_amd.dist.FrameConfig field (A/B runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: every CPU this process may use, see host_cores)")
@@ -195,6 +197,11 @@ def main():
     cfg = pmdist.FrameConfig(casted=casted_total, caustic=caustic_total, max_depth=args.max_depth,
                              width=args.width, height=args.height, spp=args.spp, depth=args.depth, sky=SKY,
                              camera=CAMERA, caustic_k=args.caustic_k)
+    for opt in args.frame_opt:
+        field, _, v = opt.partition("=")
+        if not isinstance(getattr(cfg, field, None), bool) or v not in ("0", "1"):
+            raise SystemExit(f"--frame-opt: {opt!r} is not FIELD=0|1 for a boolean FrameConfig field")
+        setattr(cfg, field, v == "1")
     backend = pmdist.GpuBackend(scene, lights, cfg, rank, world, gbuf=gbuf, cbuf=cbuf)
 
     def step():

@@ -278,6 +278,12 @@ int pm_render_begin(pm_scene* scene, const pm_render_params* params,
 int pm_render_finish(pm_render_job* job, const pm_photon_map* global_map,
                      const pm_photon_map* caustic_map, uint32_t* d_rgba,
                      float* d_rgb, void* stream);
+/* Optional, between begin and finish: run the job's caustic gather now (it
+ * needs only the caustic map, e.g. beside the global map's trace and build;
+ * synchronous on `stream`). pm_render_finish then runs only the global gather
+ * and takes caustic_map = NULL or this same map. Once per job. */
+int pm_render_gather_caustic(pm_render_job* job, const pm_photon_map* caustic_map,
+                             void* stream);
 int pm_render_job_destroy(pm_render_job* job);
 
 /* ---- photon viewer (photon-viewer/; debug splat) --------

@@ -48,6 +48,8 @@ const pm_render_stats& render_job_stats(const pm_render_job* J);
 pm_scene* render_job_scene(const pm_render_job* J);
 bool render_job_finished(const pm_render_job* J);
 void render_job_mark_finished(pm_render_job* J);
+const pm_photon_map* render_job_caustic_map(const pm_render_job* J);
+hipError_t render_gather_caustic(pm_render_job* J, const pm_photon_map* cmap, hipStream_t s);
 
 namespace {
 std::mutex g_phase_mu;   // guards g_render_stats
@@ -408,6 +410,7 @@ int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_phot
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
   pm_photon_map* m = new pm_photon_map;
+  m->made_on = s;
   m->n = n;
   if (n > 0) {
     m->nodes.alloc(n);
@@ -449,7 +452,12 @@ int pm_photon_map_export(const pm_photon_map* m, pm_kd_photon* d_out, void* stre
 }
 
 int pm_photon_map_destroy(pm_photon_map* m) {
-  delete m;
+  if (m) {
+    // back to the pool of the stream it was built on (a map built on a side
+    // stream every frame would otherwise hipMalloc anew each time)
+    AllocStream pool(m->made_on);
+    delete m;
+  }
   return PM_OK;
 }
 
@@ -539,6 +547,7 @@ int pm_photon_map_create_sharded(pm_kd_shard_plan* p, const int32_t* subs, pm_ph
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
   pm_photon_map* m = new pm_photon_map;
+  m->made_on = s;
   m->n = p->n;
   hipError_t e = hipSuccess;
   if (p->n > 0) {
@@ -661,9 +670,23 @@ int pm_render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lig
   return PM_OK;
 }
 
+int pm_render_gather_caustic(pm_render_job* J, const pm_photon_map* cmap, void* stream) {
+  if (!J || !cmap || render_job_finished(J) || render_job_caustic_map(J)) return PM_ERR_INVALID;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  reset_phase(PH_GATHER);
+  {
+    PhaseTimer tm(PH_GATHER, s);
+    PM_TRY_ST(render_gather_caustic(J, cmap, s));
+  }
+  return PM_OK;
+}
+
 int pm_render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba,
                      float* rgb, void* stream) {
-  if (!J || !gmap || !cmap || !rgba || render_job_finished(J)) return PM_ERR_INVALID;
+  if (!J || !gmap || !rgba || render_job_finished(J)) return PM_ERR_INVALID;
+  const pm_photon_map* early = render_job_caustic_map(J);
+  if (early ? (cmap && cmap != early) : !cmap) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
   reset_phase(PH_GATHER); reset_phase(PH_RESOLVE); reset_phase(PH_GATHER_GLOBAL);

@@ -36,6 +36,7 @@ struct pm_photon_map {
   pmd::DevBuf<float4> nodes;
   pmd::DevBuf<float4> payload;
   int64_t n = 0;
+  hipStream_t made_on = nullptr;   // its memory returns to this stream's allocator pool
 };
 
 // PM_CHECK_VARIANT (build-time, tests only: lib_check/libpm_hip.so): every

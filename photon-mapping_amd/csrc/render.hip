@@ -560,6 +560,7 @@ struct pm_render_job {
   bool finished = false;
   hipStream_t side = nullptr;   // the caustic gather's stream (render_finish), created on first use
   hipStream_t begun_on = nullptr;   // render_begin's stream: the job's buffers return to its allocator pool
+  const pm_photon_map* caustic_map = nullptr;   // set once the caustic gather ran (render_gather_caustic)
   ~pm_render_job() {
     if (side) (void)hipStreamDestroy(side);
   }
@@ -588,6 +589,7 @@ const pm_render_stats& render_job_stats(const pm_render_job* J) { return J->stat
 pm_scene* render_job_scene(const pm_render_job* J) { return J->scene; }
 bool render_job_finished(const pm_render_job* J) { return J->finished; }
 void render_job_mark_finished(pm_render_job* J) { J->finished = true; }
+const pm_photon_map* render_job_caustic_map(const pm_render_job* J) { return J->caustic_map; }
 
 hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lights, int nl, pm_render_job* J,
                         hipStream_t s) {
@@ -741,41 +743,58 @@ hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light*
   return hipSuccess;
 }
 
+// The caustic gather alone, ahead of render_finish: it needs only the caustic
+// map, so a frame can run it beside the global map's trace and build.
+hipError_t render_gather_caustic(pm_render_job* J, const pm_photon_map* cmap, hipStream_t s) {
+  if (J->nthreads > 0) {
+    PM_HIP_TRY(gather_sorted(cmap, J->cs, J->cres.p, 0, s, J->A.caustic_k));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+  }
+  J->caustic_map = cmap;
+  return hipSuccess;
+}
+
 hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_photon_map* cmap, uint32_t* rgba,
                          float* rgb, hipStream_t s) {
   if (J->nthreads == 0) return hipSuccess;
   {
-    // The two gathers are independent: the caustic one runs on a side stream
-    // beside the global one. The global map's leader launch (every 16th
-    // query) ends with its slowest waves while most of the GPU idles -- on the
-    // Cornell box (config 2) 231k leaders, fewer waves than the GPU holds, and
-    // a few leaders walk thousands of nodes -- and the caustic gather fills it.
+    // The two gathers are independent: unless render_gather_caustic already
+    // ran it, the caustic one runs on a side stream beside the global one. The
+    // global map's leader launch (every 16th query) ends with its slowest
+    // waves while most of the GPU idles -- on the Cornell box (config 2) 231k
+    // leaders, fewer waves than the GPU holds, and a few leaders walk
+    // thousands of nodes -- and the caustic gather fills it.
     // The global gather is enqueued first: a k != 50 caustic gather
     // synchronises its own stream before it returns.
     // (The global gather's own time comes from events read after the final
     // synchronisation: a host wait between the two would serialise them.)
     PhaseTimer tm(PH_GATHER, s);
-    if (!J->side) PM_HIP_TRY(hipStreamCreateWithFlags(&J->side, hipStreamNonBlocking));
+    const bool side = J->caustic_map == nullptr;
+    if (side && !J->side) PM_HIP_TRY(hipStreamCreateWithFlags(&J->side, hipStreamNonBlocking));
     hipEvent_t ready = nullptr, done = nullptr, g0 = nullptr, g1 = nullptr;
-    hipError_t e = hipEventCreateWithFlags(&ready, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreate(&g0);
+    hipError_t e = hipEventCreate(&g0);
     if (e == hipSuccess) e = hipEventCreate(&g1);
-    if (e == hipSuccess) e = hipEventRecord(ready, s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(J->side, ready, 0);
+    if (side) {
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventRecord(ready, s);
+      if (e == hipSuccess) e = hipStreamWaitEvent(J->side, ready, 0);
+    }
     if (e == hipSuccess) e = hipEventRecord(g0, s);
     if (e == hipSuccess) e = gather_sorted(gmap, J->gs, J->gres.p, 1, s);
     if (e == hipSuccess) e = hipEventRecord(g1, s);
-    if (e == hipSuccess) {
-      AllocStream side_pool(J->side);   // the side gather's temporaries belong to its stream
-      e = gather_sorted(cmap, J->cs, J->cres.p, 0, J->side, J->A.caustic_k);
+    if (side) {
+      if (e == hipSuccess) {
+        AllocStream side_pool(J->side);   // the side gather's temporaries belong to its stream
+        e = gather_sorted(cmap, J->cs, J->cres.p, 0, J->side, J->A.caustic_k);
+      }
+      if (e == hipSuccess) e = hipEventRecord(done, J->side);
+      if (e == hipSuccess) e = hipStreamWaitEvent(s, done, 0);
     }
-    if (e == hipSuccess) e = hipEventRecord(done, J->side);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, done, 0);
     if (e == hipSuccess) e = hipEventSynchronize(g1);
     float ms = 0.f;
     if (e == hipSuccess && hipEventElapsedTime(&ms, g0, g1) == hipSuccess) record_phase_us(PH_GATHER_GLOBAL, ms * 1e3);
-    if (e != hipSuccess) (void)hipStreamSynchronize(J->side);   // no side work outlives a failed call
+    if (e != hipSuccess && side) (void)hipStreamSynchronize(J->side);   // no side work outlives a failed call
     for (hipEvent_t ev : {ready, done, g0, g1})
       if (ev) (void)hipEventDestroy(ev);
     PM_HIP_TRY(e);

@@ -171,6 +171,7 @@ _SIGNATURES = {
     "pm_render_begin": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Light), C.c_int32, C.POINTER(_P), _P]),
     "pm_render_finish": (C.c_int, [_P, _P, _P, _P, _P, _P]),
     "pm_render_job_destroy": (C.c_int, [_P]),
+    "pm_render_gather_caustic": (C.c_int, [_P, _P, _P]),
     "pm_photon_view": (C.c_int, [_P, _P, C.c_int64, C.POINTER(ViewerParams), _P, _P]),
     "pm_config_load": (C.c_int, [C.c_char_p, C.POINTER(Config)]),
     "pm_config_key_name": (C.c_char_p, [C.c_int32]),
@@ -625,13 +626,20 @@ class RenderJob:
                "pm_render_begin")
         self._h = h.value
 
-    def finish(self, global_map: PhotonMap, caustic_map: PhotonMap, want_rgb: bool = True, rgba=None, stream=None):
+    def gather_caustic(self, caustic_map: PhotonMap, stream=None):
+        """pm_render_gather_caustic: the caustic gather now, ahead of finish()
+        (which then takes caustic_map=None or this same map)."""
+        _check(_lib.pm_render_gather_caustic(self._h, caustic_map.handle, _stream(stream)),
+               "pm_render_gather_caustic")
+
+    def finish(self, global_map: PhotonMap, caustic_map: Optional[PhotonMap], want_rgb: bool = True, rgba=None,
+               stream=None):
         import torch
         if rgba is None:
             rgba = torch.zeros((self.height, self.width), dtype=torch.int32, device="cuda")
         rgb = torch.zeros((self.height, self.width, 3), dtype=torch.float32, device="cuda") if want_rgb else None
-        _check(_lib.pm_render_finish(self._h, global_map.handle, caustic_map.handle, _ptr(rgba), _ptr(rgb),
-                                     _stream(stream)), "pm_render_finish")
+        _check(_lib.pm_render_finish(self._h, global_map.handle, caustic_map.handle if caustic_map else None,
+                                     _ptr(rgba), _ptr(rgb), _stream(stream)), "pm_render_finish")
         return rgba, rgb
 
     def close(self):

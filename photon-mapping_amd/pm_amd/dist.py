@@ -284,20 +284,26 @@ class GpuBackend:
         self.phase["kdbuild"] = self.phase.get("kdbuild", 0.0) + kd
         return gm
 
-    def start_render(self, tile_rank: int, tile_count: int, caustic_shard=None):
+    def start_render(self, tile_rank: int, tile_count: int, caustic_shard=None, caustic_map: bool = False):
         """pm_render_begin on a side stream from a second host thread; returns a
         handle for finish_render. The begin half synchronises its stream before
         it returns, so the job is complete once the thread has ended. With
         caustic_shard=(rank, world) the same thread then traces the caustic
         photons on that stream (take them with caustic_photons): its short,
         latency-bound bounce launches fill the GPU beside the global trace's
-        tail instead of running after it."""
+        tail instead of running after it. With caustic_map as well (one rank,
+        no quantisation: the map is then built from these photons alone) it
+        also builds the caustic map there (take it with caustic_map_of). The
+        caustic gather stays in finish_render, on a side stream beside the
+        global gather's leader launch: run here (pm_render_gather_caustic) it
+        landed beside the kd build (config 3: kd 25.3 -> 28 ms, frame
+        unchanged) and, on the Cornell box, held the global gather back."""
         import threading
         import torch
         pm, c = self.pm, self.cfg
         if getattr(self, "_rside", None) is None:
             self._rside = torch.cuda.Stream()
-        side, box = self._rside, {}
+        side, box = self._rside, {"c_ready": threading.Event()}
 
         def run():
             try:
@@ -310,8 +316,14 @@ class GpuBackend:
                                                    shard_rank=caustic_shard[0], shard_count=caustic_shard[1],
                                                    out=self.cbuf, stream=side.cuda_stream)
                     box["c"] = (t, pm.phase_us("trace") + pm.phase_us("compact"))
+                    box["c_ready"].set()   # the main thread goes on; the map and gather follow here
+                    if caustic_map:
+                        cm = pm.PhotonMap(t, pm.CAUSTICS_PHOTON_POWER, stream=side.cuda_stream)
+                        box["cm"] = (cm, pm.phase_us("kdbuild"))
             except BaseException as e:   # re-raised by finish_render / join_render
                 box["e"] = e
+            finally:
+                box["c_ready"].set()
 
         th = threading.Thread(target=run, name="pm-render-begin")
         th.start()
@@ -319,11 +331,23 @@ class GpuBackend:
 
     def caustic_photons(self, pending):
         """The caustic photons traced by start_render(caustic_shard=...)'s thread
-        (complete: the thread synchronised its stream)."""
-        self.join_render(pending)
-        t, us = pending[1]["c"]
+        (complete: the thread synchronised its stream before signalling). Does
+        not wait for the thread's caustic map and gather."""
+        box = pending[1]
+        box["c_ready"].wait()
+        if "c" not in box:
+            self.join_render(pending)   # re-raises the thread's error
+        t, us = box["c"]
         self.phase["trace"] = self.phase.get("trace", 0.0) + us
         return t
+
+    def caustic_map_of(self, pending):
+        """The caustic map start_render(caustic_map=True)'s thread built (waits
+        for the thread)."""
+        self.join_render(pending)
+        cm, kd_us = pending[1]["cm"]
+        self.phase["kdbuild"] = self.phase.get("kdbuild", 0.0) + kd_us
+        return cm
 
     @staticmethod
     def join_render(pending):
@@ -365,9 +389,10 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     backend.phase = {}
     pending = None
     if backend.cfg.overlap_render and hasattr(backend, "start_render"):
-        pending = backend.start_render(rank, world, caustic_shard=(rank, world))
+        early_caustic = world == 1 and not backend.cfg.quantize
+        pending = backend.start_render(rank, world, caustic_shard=(rank, world), caustic_map=early_caustic)
     try:
-        g, c, gm, cm = _maps(backend, rank, world, dist, pending)
+        g, c, gm, cm = _maps(backend, rank, world, dist, pending, pending is not None and early_caustic)
     except BaseException:
         if pending is not None:   # no side work outlives a failed frame
             try:
@@ -378,6 +403,8 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     if world > 1 and rgba is not None:
         rgba.zero_()   # tiles are disjoint: the SUM-reduce needs zeros outside this rank's tiles
     if pending is not None:
+        if cm is None:
+            cm = backend.caustic_map_of(pending)
         rgba = backend.finish_render(pending, gm, cm, rgba)
     else:
         rgba = backend.render(gm, cm, rank, world, rgba)
@@ -388,10 +415,11 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     return rgba, info
 
 
-def _maps(backend, rank: int, world: int, dist, pending=None):
+def _maps(backend, rank: int, world: int, dist, pending=None, early_caustic: bool = False):
     """Trace both photon sets, exchange them (N > 1), build both maps. With a
     render pending from start_render(caustic_shard=...), the caustic photons
-    come from its thread."""
+    come from its thread; with early_caustic (world 1), so does the caustic map
+    (returned as None here)."""
     g = backend.trace(False, rank, world)
     c = backend.caustic_photons(pending) if pending is not None else backend.trace(True, rank, world)
     if backend.cfg.quantize:   # elementwise: the same before or after the exchange
@@ -401,12 +429,13 @@ def _maps(backend, rank: int, world: int, dist, pending=None):
         # 24 of the 40 bytes of a photon cross xGMI
         clock = _PhaseClock(g.device.type == "cuda")
         c = unpack_rows(allgather_rows(pack_rows(c), world, dist))
-        pending = allgather_rows_start(pack_rows(g), world, dist)
+        xfer = allgather_rows_start(pack_rows(g), world, dist)
         cm = backend.caustic_map(c)   # overlaps the global photons' transfer
-        g = unpack_rows(pending.wait())
+        g = unpack_rows(xfer.wait())
         backend.phase["exchange"] = clock.stop_us()
     else:
         backend.phase["exchange"] = 0.0
-        cm = backend.caustic_map(c)
+        # None: start_render's thread builds it (frame() takes it before the render)
+        cm = None if early_caustic else backend.caustic_map(c)
     gm = backend.global_map(g, c, rank, world, dist)
     return g, c, gm, cm

@@ -390,6 +390,24 @@ def test_render_begin_finish_equals_render(cornell):
     with pytest.raises(pm_amd.PMError):
         job.finish(gmap, cmap)
     job.close()
+    # the caustic gather ahead of finish (pm_render_gather_caustic, on the side
+    # stream): finish then takes no caustic map, or the same one, not another
+    for again in (None, cmap):
+        job = pm_amd.render_begin(gs, cam, W, H, 2, 30, (1, 1, 1), lights, stream=side.cuda_stream)
+        job.gather_caustic(cmap, stream=side.cuda_stream)
+        with pytest.raises(pm_amd.PMError):
+            job.gather_caustic(cmap)   # once per job
+        with pytest.raises(pm_amd.PMError):
+            job.finish(gmap, gmap)   # not the map it gathered
+        rgba3, rgb3 = job.finish(gmap, again)
+        assert torch.equal(rgba, rgba3)
+        assert np.array_equal(_bits(rgb.cpu().numpy()), _bits(rgb3.cpu().numpy()))
+        assert bytes(st) == bytes(pm_amd.render_stats())
+        job.close()
+    job = pm_amd.render_begin(gs, cam, W, H, 2, 30, (1, 1, 1), lights)
+    with pytest.raises(pm_amd.PMError):
+        job.finish(gmap, None)   # no caustic map and none gathered
+    job.close()
 
 
 def test_frame_driver_matches_direct_pipeline(cornell):
