@@ -464,9 +464,72 @@ static hipError_t gather_sorted(const pm_photon_map* m, SortedQueries& Q, float4
   return hipSuccess;
 }
 
-__global__ __launch_bounds__(256) void k_resolve(RenderArgs A, PathOut O, const uint32_t* cidx, const float4* cres,
-                                                 const uint32_t* gidx, const float4* gres, uint32_t* rgba,
-                                                 float* rgb) {
+// Per-vertex colour (deviceCode.cu:173-231's vertex term): the 20 final-gather
+// samples of 64 consecutive vertices are read by the whole block (flags,
+// albedo, gather result: consecutive lanes, consecutive samples), their
+// products staged in LDS, then one lane per vertex sums them in sample order,
+// exactly as the per-pixel walk did. (One lane per vertex reading its own
+// 80-B flag row and 320-B albedo row, 64 rows apart across the wave, made the
+// old single-kernel resolve ~1 ms for ~1.6 GB.)
+constexpr int kVcVerts = 64;
+constexpr int kVcSamples = kVcVerts * kNumDiffuseSamples;
+__global__ __launch_bounds__(256) void k_vertex_colour(PathOut O, int64_t nv, const uint32_t* __restrict__ cidx,
+                                                       const float4* __restrict__ cres,
+                                                       const uint32_t* __restrict__ gidx,
+                                                       const float4* __restrict__ gres, float4* __restrict__ vcol) {
+  __shared__ float prod[3][kVcSamples];
+  __shared__ uint8_t pvalid[kVcSamples];
+  const int64_t v0 = (int64_t)blockIdx.x * kVcVerts;
+  const int64_t nvb = nv - v0 < kVcVerts ? nv - v0 : kVcVerts;
+  const int64_t ns = nvb * kNumDiffuseSamples;
+  for (int i = threadIdx.x; i < kVcSamples; i += blockDim.x) {
+    uint32_t ok = 0;
+    if (i < ns) {
+      const int64_t gi = v0 * kNumDiffuseSamples + i;
+      ok = O.gvalid[gi];
+      if (ok) {
+        const float4 g4 = gres[gidx[gi]];   // valid samples are consecutive in gres
+        const float4 al = O.galb[gi];
+        const v3 p = mulv(v3{g4.x, g4.y, g4.z}, v3{al.x, al.y, al.z});
+        prod[0][i] = p.x;
+        prod[1][i] = p.y;
+        prod[2][i] = p.z;
+      }
+    }
+    pvalid[i] = (uint8_t)ok;
+  }
+  __syncthreads();
+  const int lv = threadIdx.x;
+  if (lv >= nvb) return;
+  const int64_t v = v0 + lv;
+  const uint32_t fl = O.vflags[v];
+  v3 c;
+  if (fl & VF_MISS) {
+    const float4 sk = O.vdirect[v];
+    c = {sk.x, sk.y, sk.z};
+  } else {
+    const float4 c4 = cres[cidx[v]];
+    const v3 caustics = {c4.x, c4.y, c4.z};
+    v3 diffuse = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < kNumDiffuseSamples; j++) {
+      const int i = lv * kNumDiffuseSamples + j;
+      if (pvalid[i]) diffuse = add(diffuse, v3{prod[0][i], prod[1][i], prod[2][i]});
+    }
+    diffuse = divf(diffuse, (float)kNumDiffuseSamples);
+    const float4 ab = O.valb[v];
+    diffuse = mulv(diffuse, v3{ab.x, ab.y, ab.z});
+    const float4 d4 = O.vdirect[v];
+    c = {kDiffuseFactor * diffuse.x + kCausticsFactor * caustics.x + kDirectLightFactor * d4.x,
+         kDiffuseFactor * diffuse.y + kCausticsFactor * caustics.y + kDirectLightFactor * d4.y,
+         kDiffuseFactor * diffuse.z + kCausticsFactor * caustics.z + kDirectLightFactor * d4.z};
+  }
+  vcol[v] = make_float4(c.x, c.y, c.z, 0.f);
+}
+
+// ray_colour's accumulation along each camera path: colour += c_v * att_v.
+__global__ __launch_bounds__(256) void k_resolve(RenderArgs A, PathOut O, const float4* __restrict__ vcol,
+                                                 uint32_t* rgba, float* rgb) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int px, py;
   if (!pixel_of(A, tid, px, py)) return;
@@ -476,51 +539,8 @@ __global__ __launch_bounds__(256) void k_resolve(RenderArgs A, PathOut O, const 
     for (int64_t v = tid * A.spp + s; v >= 0;) {
       const uint32_t fl = O.vflags[v];
       const float4 a4 = O.vatt[v];
-      const v3 att = {a4.x, a4.y, a4.z};
-      v3 c;
-      if (fl & VF_MISS) {
-        const float4 sk = O.vdirect[v];
-        c = {sk.x, sk.y, sk.z};
-      } else {
-        const float4 c4 = cres[cidx[v]];
-        const v3 caustics = {c4.x, c4.y, c4.z};
-        v3 diffuse = {0.f, 0.f, 0.f};
-        // this vertex's 20 sample flags as five 16-B loads (rows are 80 B, 16-B
-        // aligned): per-lane scalar loads 80 B apart thrashed L1/L2 (~16 GB of
-        // fetches per launch). Valid samples are consecutive in gres.
-        static_assert(kNumDiffuseSamples % 4 == 0, "vector rows");
-        uint32_t gv[kNumDiffuseSamples];
-        const uint4* gv4 = reinterpret_cast<const uint4*>(O.gvalid + v * kNumDiffuseSamples);
-#pragma unroll
-        for (int k = 0; k < kNumDiffuseSamples / 4; k++) {
-          const uint4 t = gv4[k];
-          gv[4 * k] = t.x; gv[4 * k + 1] = t.y; gv[4 * k + 2] = t.z; gv[4 * k + 3] = t.w;
-        }
-        bool anyv = false;
-#pragma unroll
-        for (int j = 0; j < kNumDiffuseSamples; j++) anyv |= gv[j] != 0u;
-        if (anyv) {
-          uint32_t r = 0xFFFFFFFFu;
-#pragma unroll
-          for (int j = 0; j < kNumDiffuseSamples; j++)
-            if (gv[j] && r == 0xFFFFFFFFu) r = gidx[v * kNumDiffuseSamples + j];
-#pragma unroll
-          for (int j = 0; j < kNumDiffuseSamples; j++) {
-            if (!gv[j]) continue;
-            const float4 g4 = gres[r++];
-            const float4 al = O.galb[v * kNumDiffuseSamples + j];
-            diffuse = add(diffuse, mulv(v3{g4.x, g4.y, g4.z}, v3{al.x, al.y, al.z}));
-          }
-        }
-        diffuse = divf(diffuse, (float)kNumDiffuseSamples);
-        const float4 ab = O.valb[v];
-        diffuse = mulv(diffuse, v3{ab.x, ab.y, ab.z});
-        const float4 d4 = O.vdirect[v];
-        c = {kDiffuseFactor * diffuse.x + kCausticsFactor * caustics.x + kDirectLightFactor * d4.x,
-             kDiffuseFactor * diffuse.y + kCausticsFactor * caustics.y + kDirectLightFactor * d4.y,
-             kDiffuseFactor * diffuse.z + kCausticsFactor * caustics.z + kDirectLightFactor * d4.z};
-      }
-      colour = add(colour, mulv(c, att));
+      const float4 c4 = vcol[v];
+      colour = add(colour, mulv(v3{c4.x, c4.y, c4.z}, v3{a4.x, a4.y, a4.z}));
       if (fl & VF_LAST) break;
       v = O.next[v];
     }
@@ -804,9 +824,16 @@ hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_p
             J->nbase,     J->cap};
   {
     PhaseTimer tm(PH_RESOLVE, s);
-    k_resolve<<<grid_for(J->nthreads, 256), 256, 0, s>>>(J->A, O, J->cidx.p, J->cres.p, J->gidx.p, J->gres.p, rgba,
-                                                         rgb);
+    DevBuf<float4> vcol(J->NV);
+    if (J->NV > 0 && !vcol.p) return hipErrorOutOfMemory;
+    if (J->NV > 0) {
+      k_vertex_colour<<<(int)((J->NV + kVcVerts - 1) / kVcVerts), 256, 0, s>>>(O, J->NV, J->cidx.p, J->cres.p,
+                                                                               J->gidx.p, J->gres.p, vcol.p);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    k_resolve<<<grid_for(J->nthreads, 256), 256, 0, s>>>(J->A, O, vcol.p, rgba, rgb);
     PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(hipStreamSynchronize(s));   // vcol is freed on scope exit
   }
   return hipStreamSynchronize(s);
 }
