@@ -279,26 +279,35 @@ __device__ __forceinline__ void lean_round(double (&list)[K], LeanWalk& w, const
   w.bound = gkey_d2(list[K - 1]);
 }
 
-template <int K, int QL, bool WIDE>
-__device__ __forceinline__ void knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float cut, bool valid,
+// BUDGET > 0: the walk stops after BUDGET wave iterations; lanes still walking
+// then are reported (return value) and their lists are incomplete.
+template <int K, int QL, bool WIDE, int BUDGET = 0>
+__device__ __forceinline__ bool knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float cut, bool valid,
                                               double (&list)[K], double* lq, int lstride) {
   const double sentinel = gkey(cut, kNoWord);
 #pragma unroll
   for (int j = 0; j < K; j++) list[j] = sentinel;
-  if (n <= 0) return;   // empty map: every lane keeps the sentinel list (uniform)
+  if (n <= 0) return false;   // empty map: every lane keeps the sentinel list (uniform)
   LeanWalk w;
   w.start(cut, valid);
   w.qn = 0;
   lq[0] = __longlong_as_double(0x7FEFFFFFFFFFFFFFll);   // slot 0: DBL_MAX, never inserted
   float4 nd = node1<WIDE>(nodes, 1);
+  bool aborted = false;
+  int it = 0;   // wave-uniform
   for (;;) {
     lean_step<K, WIDE>(nodes, (uint32_t)n, q, list[K - 1], w, nd, lq, lstride);
+    if (BUDGET > 0 && ++it == BUDGET) {
+      aborted = w.walking;
+      w.walking = false;
+    }
     const bool any_walking = ballot(w.walking) != 0;
     if (ballot(w.qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
       lean_round<K>(list, w, lq, lstride);
       if (!any_walking && ballot(w.qn > 0) == 0) break;
     }
   }
+  return aborted;
 }
 
 // pm_knn: K-wide list for k <= K; k > 128 runs 128-wide passes (j0 = output
@@ -395,6 +404,19 @@ __device__ __forceinline__ v3 radiance_g(const double (&list)[kKNearest], const 
 constexpr int kSeedStride = PM_SEED_STRIDE;
 constexpr int kSeedLeaders = PM_SEED_LEADERS;
 constexpr int kGatherQL = PM_GATHER_QL;   // LDS insert-queue depth
+// Leader step budget (wave iterations; 0: none). A leader wave ends when its
+// lanes are done or after this many iterations; a lane still walking then
+// (on the Cornell box, depth-first walks that wander through planar walls:
+// up to ~78k steps, while most leader waves need a few hundred) writes no seed
+// record and is re-walked, without a budget, by the first workgroups of the
+// follower launch -- beside the followers instead of
+// before them. Results are unchanged (a cut-off only prunes; the retry walk
+// is the leader walk). The retry workgroups come first in the launch, so the
+// long walks start before (and overlap) the follower workgroups.
+#ifndef PM_LEADER_BUDGET
+#define PM_LEADER_BUDGET 8192
+#endif
+constexpr int kLeaderBudget = PM_LEADER_BUDGET;
 
 __device__ __forceinline__ double seed_bound(float4 lead, v3 q) {
   if (!(lead.w >= 0.f)) return 1e300;
@@ -475,24 +497,53 @@ __device__ __forceinline__ float subtree_cut(const float4* __restrict__ nodes, u
 template <int TAG, bool LEADERS, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
-    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead) {
+    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
+    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks) {
   __shared__ double lq[(kGatherQL + 1) * 256];
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
-  const bool valid = r < nq;
+  const float R2 = kKMaxDistance * kKMaxDistance;
+  // follower launch with a leader budget: the first nretry_blocks workgroups
+  // (one lane per leader) re-walk the leaders that ran out of budget, with the
+  // leaders' own cut-off; the walk and the epilogue are shared
+  const int64_t nrb = (!LEADERS && nretry) ? (int64_t)retry_blocks : 0;
+  const bool redo_lane = (int64_t)blockIdx.x < nrb;
+  int64_t r;
+  bool valid;
+  if (redo_lane) {
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    valid = e < *nretry;
+    r = valid ? (int64_t)retry[e] : 0;
+  } else {
+    const int64_t t = ((int64_t)blockIdx.x - nrb) * blockDim.x + threadIdx.x;
+    r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
+    valid = r < nq;
+  }
+  if (redo_lane && ballot(valid) == 0) return;   // wave-uniform: no retry entry for this wave
   const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   const v3 q = {qq.x, qq.y, qq.z};
-  const float R2 = kKMaxDistance * kKMaxDistance;
   float cut = lean_cut(R2);
-  if (valid) cut = LEADERS ? subtree_cut<WIDE>(nodes, (uint32_t)n, q, cut) : follower_cut(lead, nq, r, q, R2);
+  if (valid)
+    cut = (LEADERS || redo_lane) ? subtree_cut<WIDE>(nodes, (uint32_t)n, q, cut) : follower_cut(lead, nq, r, q, R2);
   double list[kKNearest];
-  knn_walk_lean<kKNearest, kGatherQL, WIDE>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
-  if (valid) {
+  const bool aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0>(
+      nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
+  if (valid && !aborted) {
     const bool full = gkey_word(list[kKNearest - 1]) != kNoWord;
     const v3 f = radiance_g(list, payload, qq.w, full ? gkey_d2(list[kKNearest - 1]) : R2);
     out[i] = make_float4(f.x, f.y, f.z, 0.f);
     if (LEADERS) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, full ? gkey_d2(list[kKNearest - 1]) : -1.f);
+  }
+  if (LEADERS && kLeaderBudget > 0) {
+    const bool redo = valid && aborted;
+    if (redo) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, -1.f);   // seeds nothing
+    const uint64_t m = ballot(redo);
+    if (m != 0) {   // wave-aggregated append to the retry list
+      const int lane = threadIdx.x & 63, first = __ffsll((long long)m) - 1;
+      uint32_t base = 0;
+      if (lane == first) base = atomicAdd(nretry, (uint32_t)__popcll(m));
+      base = __shfl(base, first);
+      if (redo) retry[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint32_t)r;
+    }
   }
 }
 
@@ -576,14 +627,21 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
 #else
   const int64_t nl = (nq + kSeedStride - 1) / kSeedStride;   // leaders: walk ranks 0, S, 2S, ...
   DevBuf<float4> lead(nl);
-  if (!lead.p) return hipErrorOutOfMemory;
-  const int gl = grid_for(nl, 256), gf = grid_for(nq - nl, 256);
+  DevBuf<uint32_t> retry(kLeaderBudget > 0 ? nl : 0), nretry(kLeaderBudget > 0 ? 1 : 0);
+  if (!lead.p || (kLeaderBudget > 0 && (!retry.p || !nretry.p))) return hipErrorOutOfMemory;
+  if (kLeaderBudget > 0) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, sizeof(uint32_t), s));
+  // followers (+ the retry workgroups first, with a leader budget)
+  const int rb = kLeaderBudget > 0 ? grid_for(nl, 256) : 0;   // retry workgroups: one lane per leader
+  const int gl = grid_for(nl, 256), gf = grid_for(nq - nl, 256) + rb;
   // node byte offsets fit 32 bits below 2^28 nodes (saddr loads); larger maps use 64-bit addresses
   const bool wide = n >= (1 << 28);
 #define PM_LEVELS(T, W)                                                                                          \
-  k_gather_level<T, true, W><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p);       \
+  k_gather_level<T, true, W><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, retry.p, \
+                                                nretry.p, 0);                                                   \
   PM_HIP_TRY(hipGetLastError());                                                                                \
-  if (nq > nl) k_gather_level<T, false, W><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p)
+  if (nq > nl || kLeaderBudget > 0)                                                                             \
+  k_gather_level<T, false, W><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, retry.p, \
+                                                 nretry.p, rb)
   if (tag == 1) {
     if (wide) {
       PM_LEVELS(1, true);

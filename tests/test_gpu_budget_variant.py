@@ -1,0 +1,51 @@
+"""The gather's leader-budget retry path against the production library.
+
+lib_budget/libpm_hip.so is built with PM_LEADER_BUDGET=4 (photon-mapping_amd/
+Makefile `budget`, built by __graft_entry__.build()): a leader wave stops after
+4 walk iterations, so nearly every leader writes no seed record and is re-walked
+by the retry workgroups at the head of the follower launch (csrc/knn.hip,
+k_gather_level), while the followers fall back to whatever leaders finished
+(none: the plain cut-off). Production uses a budget of 8192, which only the
+Cornell box's wandering leader walks reach. The lists and radiance must not
+depend on either: the small workloads of tests/variant_workloads.py (seeded
+gathers with ties and duplicates, Cornell and sphere renders) run in one child
+process with the variant and must match production bit for bit."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import conftest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+PKG = os.path.join(conftest.ROOT, "photon-mapping_amd")
+VARIANT = os.path.join(PKG, "lib_budget", "libpm_hip.so")
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+KEYS = ["gather_g", "gather_c", "gather_e", "render_64_rgba", "render_64_rgb", "render_64_stats", "render_40_rgba",
+        "render_40_rgb", "render_40_stats", "sphere_rgb", "sphere_stats"]
+
+
+@pytest.fixture(scope="module")
+def runs(tmp_path_factory):
+    assert os.path.exists(VARIANT), f"budget variant not built ({VARIANT}): run __graft_entry__.build()"
+    import variant_workloads
+    out = str(tmp_path_factory.mktemp("budget") / "budget.npz")
+    env = dict(os.environ, PM_HIP_LIB=VARIANT)
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "variant_workloads.py"), out], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "lib_budget/libpm_hip.so" in r.stdout, r.stdout
+    return variant_workloads.run(full=False), dict(np.load(out))
+
+
+@pytest.mark.parametrize("key", KEYS)
+def test_budget_variant_bitwise(runs, key):
+    prod, var = runs
+    a, b = prod[key], var[key]
+    assert a.shape == b.shape, (a.shape, b.shape)
+    assert np.array_equal(np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8)), key
