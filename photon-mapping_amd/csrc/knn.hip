@@ -412,9 +412,11 @@ constexpr int kGatherQL = PM_GATHER_QL;   // LDS insert-queue depth
 // follower launch -- beside the followers instead of
 // before them. Results are unchanged (a cut-off only prunes; the retry walk
 // is the leader walk). The retry workgroups come first in the launch, so the
-// long walks start before (and overlap) the follower workgroups.
+// long walks start before (and overlap) the follower workgroups. Budget 1024 /
+// 2048 / 4096 / 8192: config 2 24.8 / 24.8-25.1 / 25.5 / 26.5 ms per frame,
+// config 3's global gather 41.1-41.3 / 40.7 / 40.7 / 40.7 ms.
 #ifndef PM_LEADER_BUDGET
-#define PM_LEADER_BUDGET 8192
+#define PM_LEADER_BUDGET 2048
 #endif
 constexpr int kLeaderBudget = PM_LEADER_BUDGET;
 

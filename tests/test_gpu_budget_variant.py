@@ -5,8 +5,8 @@ Makefile `budget`, built by __graft_entry__.build()): a leader wave stops after
 4 walk iterations, so nearly every leader writes no seed record and is re-walked
 by the retry workgroups at the head of the follower launch (csrc/knn.hip,
 k_gather_level), while the followers fall back to whatever leaders finished
-(none: the plain cut-off). Production uses a budget of 8192, which only the
-Cornell box's wandering leader walks reach. The lists and radiance must not
+(none: the plain cut-off). Production uses a budget of 2048 wave iterations,
+which mostly the Cornell box's wandering leader walks reach. The lists and radiance must not
 depend on either: the small workloads of tests/variant_workloads.py (seeded
 gathers with ties and duplicates, Cornell and sphere renders) run in one child
 process with the variant and must match production bit for bit."""
