@@ -391,9 +391,13 @@ __device__ __forceinline__ v3 radiance_g(const double (&list)[kKNearest], const 
 // Config 3 global gather (ms), measured in round 1: stride 8 / 2 leaders 50.9,
 // 8/4 50.3, 4/2 52.2, 16/2 50.6, 16/4 49.8; leader hierarchies, XCD-contiguous
 // block ranges, pooled lanes, child-line prefetch and deeper queues measured
-// slower; the exact-cut re-walk floor was 34.4 ms.
+// slower; the exact-cut re-walk floor was 34.4 ms. Round 2,
+// with the leader budget: stride 12 / 16 / 20 / 24 / 28 gave config 2
+// 24.7-25.9 / 24.9-25.3 / 22.2-22.7 / 25.5-25.7 / 23.6 ms per frame and
+// config 3's global gather 41.3-41.4 / 40.8-41.0 / 40.6-40.9 / 41.1-41.3 /
+// 40.8 ms: 20.
 #ifndef PM_SEED_STRIDE
-#define PM_SEED_STRIDE 16
+#define PM_SEED_STRIDE 20
 #endif
 #ifndef PM_SEED_LEADERS
 #define PM_SEED_LEADERS 4
