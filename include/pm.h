@@ -18,7 +18,17 @@
  *     tensors or hipMalloc); h_ / plain pointers are host memory.
  *   - `stream` is a hipStream_t passed as void* (NULL = default stream).
  *     Calls that return a host-visible scalar (counts) synchronise the stream.
- *   - handles (pm_scene, pm_photon_map) own their device memory.
+ *   - devices: a call that takes a stream runs on THAT stream's device. For
+ *     the duration of the call it makes that device current for the calling
+ *     host thread (a thread that never chose a device is on device 0) and
+ *     restores the previous one on return, so a side thread driving GPU r's
+ *     stream allocates and launches on GPU r. A NULL stream means the calling
+ *     thread's current device. Calls without a stream (pm_scene_create,
+ *     pm_device_alloc, ...) use the calling thread's current device.
+ *   - handles (pm_scene, pm_photon_map, pm_kd_shard_plan, pm_render_job) own
+ *     their device memory and belong to the device they were created on;
+ *     passing one, or a caller's device buffer, with a stream of another
+ *     device returns PM_ERR_DEVICE (nothing is launched).
  *   - single-threaded per handle.
  * There is NO CPU fallback: every compute entry point runs HIP kernels for
  * gfx950 and fails with PM_ERR_NO_DEVICE when no GPU is present.
@@ -33,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 2
+#define PM_ABI_VERSION 3
 
 enum pm_status {
   PM_OK = 0,
@@ -43,7 +53,8 @@ enum pm_status {
   PM_ERR_NO_DEVICE = 4,   /* no gfx950 device visible                      */
   PM_ERR_IO = 5,          /* file could not be opened / parsed             */
   PM_ERR_CAPACITY = 6,    /* output buffer too small (count still written) */
-  PM_ERR_OVERFLOW = 7     /* traversal stack overflow inside a kernel      */
+  PM_ERR_OVERFLOW = 7,    /* traversal stack overflow inside a kernel      */
+  PM_ERR_DEVICE = 8       /* handle / buffer on another device than the stream */
 };
 
 typedef struct { float x, y, z; } pm_float3;
@@ -130,6 +141,10 @@ int pm_device_alloc(size_t bytes, void** d_ptr);
 int pm_device_free(void* d_ptr);
 int pm_copy_to_device(void* d_dst, const void* h_src, size_t bytes);
 int pm_copy_to_host(void* h_dst, const void* d_src, size_t bytes);
+/* The library's caching allocator on `device` (-1: all devices): bytes held by
+ * live blocks (owned by handles or in use by a running call) and by idle
+ * pooled blocks kept for reuse. Steady-state frames do not grow either. */
+int pm_device_pool_stats(int32_t device, int64_t* live_bytes, int64_t* cached_bytes);
 
 /* ---- scene (world.cpp:3-58 loadGeometry; OptiX GAS+IAS -> HIP LBVH) ------- */
 typedef struct pm_scene pm_scene;
@@ -185,7 +200,10 @@ int pm_kdtree_build(pm_kd_photon* d_photons, int64_t n, pm_box* d_bounds, void* 
 
 /* Photon map = kd-tree + gather payload, built from stage-1 photon arrays the
  * way loadPhotons does (hostCode.cu:54-99): map = a[0..na) (power_a) ++
- * b[0..nb) (power_b). Original index = position in that concatenation. */
+ * b[0..nb) (power_b). Original index = position in that concatenation.
+ * A NaN position coordinate is taken as +inf by every tree build (this one,
+ * pm_kdtree_build, the sharded build): such a photon sorts last and is never
+ * within a gather radius (cukd leaves NaN undefined). */
 typedef struct pm_photon_map pm_photon_map;
 int pm_photon_map_create(const pm_photon* d_a, int64_t na, float power_a,
                          const pm_photon* d_b, int64_t nb, float power_b,
@@ -284,6 +302,14 @@ int pm_render_finish(pm_render_job* job, const pm_photon_map* global_map,
  * and takes caustic_map = NULL or this same map. Once per job. */
 int pm_render_gather_caustic(pm_render_job* job, const pm_photon_map* caustic_map,
                              void* stream);
+/* A job's gather queries and, once pm_render_finish ran, their results:
+ * which 0 = the global map's (final-gather) queries, 1 = the caustic ones.
+ * d_queries [count][4] = (hit point xyz, brdf), d_results [count][4] =
+ * (radiance estimate xyz, 0), in the job's dense query order; either may be
+ * NULL (both NULL: *count only). Lets a caller check a frame's gathers against
+ * an independent kNN (the parity tests) or reuse them. */
+int pm_render_job_queries(const pm_render_job* job, int32_t which, float* d_queries,
+                          float* d_results, int64_t capacity, int64_t* count, void* stream);
 int pm_render_job_destroy(pm_render_job* job);
 
 /* ---- photon viewer (photon-viewer/; debug splat) --------

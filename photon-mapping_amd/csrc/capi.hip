@@ -46,6 +46,8 @@ pm_render_job* render_job_new(pm_scene* sc, hipStream_t s);
 void render_job_delete(pm_render_job* J);
 const pm_render_stats& render_job_stats(const pm_render_job* J);
 pm_scene* render_job_scene(const pm_render_job* J);
+int render_job_device(const pm_render_job* J);
+void render_job_queries(const pm_render_job* J, int which, const float4** q, const float4** res, int64_t* n);
 bool render_job_finished(const pm_render_job* J);
 void render_job_mark_finished(pm_render_job* J);
 const pm_photon_map* render_job_caustic_map(const pm_render_job* J);
@@ -116,6 +118,30 @@ int check_overflow(pm_scene* sc, hipStream_t s) {
   return ov ? PM_ERR_OVERFLOW : PM_OK;
 }
 
+// A handle belongs to the device it was created on; a call whose stream is on
+// another device is refused (PM_ERR_DEVICE) instead of launching kernels that
+// would read that GPU's memory from this one.
+#define PM_SAME_DEVICE(scope, obj)                                   \
+  do {                                                               \
+    if ((obj) && (obj)->device != (scope).dev) return PM_ERR_DEVICE; \
+  } while (0)
+
+// A caller's device pointer that lives on another device than the call's.
+bool ptr_elsewhere(const void* p, int dev) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;   // not a HIP allocation (e.g. host memory): nothing to compare
+  }
+  return a.type == hipMemoryTypeDevice && a.device != dev;
+}
+
+#define PM_PTR_DEVICE(scope, ptr)                                 \
+  do {                                                            \
+    if (ptr_elsewhere((ptr), (scope).dev)) return PM_ERR_DEVICE;  \
+  } while (0)
+
 #define PM_TRY_ST(expr)             \
   do {                              \
     int _st = map_err(expr);        \
@@ -138,6 +164,7 @@ const char* pm_status_string(int st) {
     case PM_ERR_IO: return "I/O error";
     case PM_ERR_CAPACITY: return "output capacity too small";
     case PM_ERR_OVERFLOW: return "traversal stack overflow";
+    case PM_ERR_DEVICE: return "handle or buffer on another device than the stream";
     default: return "unknown status";
   }
 }
@@ -156,6 +183,14 @@ int pm_device_count(int32_t* count) {
 int pm_last_phase_us(int32_t phase, double* us) {
   if (!us || phase < 0 || phase >= PH_COUNT) return PM_ERR_INVALID;
   *us = g_phase_us[phase];
+  return PM_OK;
+}
+
+int pm_device_pool_stats(int32_t device, int64_t* live_bytes, int64_t* cached_bytes) {
+  size_t l = 0, c = 0;
+  dev_pool_stats(device, &l, &c);
+  if (live_bytes) *live_bytes = (int64_t)l;
+  if (cached_bytes) *cached_bytes = (int64_t)c;
   return PM_OK;
 }
 
@@ -220,6 +255,7 @@ int pm_scene_create(const pm_mesh* meshes, int32_t num_meshes, pm_scene** out) {
   }
   if (gid >= (1ll << 31)) return PM_ERR_INVALID;
   pm_scene* sc = new pm_scene;
+  sc->device = stream_device(nullptr);
   sc->ntri = (int32_t)gid;
   sc->nmesh = num_meshes;
   for (int m = 0; m < num_meshes; m++) sc->host_mat.push_back(meshes[m].material);
@@ -258,7 +294,10 @@ int pm_scene_stats_get(const pm_scene* sc, pm_scene_stats* o) {
 }
 
 int pm_scene_destroy(pm_scene* sc) {
-  delete sc;
+  if (sc) {
+    AllocStream pool(nullptr, sc->device);
+    delete sc;
+  }
   return PM_OK;
 }
 
@@ -266,6 +305,9 @@ int pm_scene_intersect(pm_scene* sc, const pm_ray* rays, int64_t n, pm_hit* hits
   if (!sc || n < 0 || (n > 0 && (!rays || !hits))) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, sc);
+  PM_PTR_DEVICE(alloc_scope, rays);
+  PM_PTR_DEVICE(alloc_scope, hits);
   PM_TRY_ST(launch_query(sc, rays, n, hits, nullptr, false, s));
   return check_overflow(sc, s);
 }
@@ -274,6 +316,9 @@ int pm_scene_occluded(pm_scene* sc, const pm_ray* rays, int64_t n, int32_t* occ,
   if (!sc || n < 0 || (n > 0 && (!rays || !occ))) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, sc);
+  PM_PTR_DEVICE(alloc_scope, rays);
+  PM_PTR_DEVICE(alloc_scope, occ);
   PM_TRY_ST(launch_query(sc, rays, n, nullptr, occ, true, s));
   return check_overflow(sc, s);
 }
@@ -330,6 +375,8 @@ int pm_trace_photons(pm_scene* sc, const pm_light* lights, int32_t nl, const pm_
   if (st != PM_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, sc);
+  PM_PTR_DEVICE(alloc_scope, d_out);
   reset_phase(PH_TRACE);
   reset_phase(PH_COMPACT);
   const int maxd = p->max_depth;
@@ -394,6 +441,8 @@ int pm_kdtree_build(pm_kd_photon* d, int64_t n, pm_box* bounds, void* stream) {
   if (st != PM_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_PTR_DEVICE(alloc_scope, d);
+  PM_PTR_DEVICE(alloc_scope, bounds);
   reset_phase(PH_KDBUILD);
   PhaseTimer tm(PH_KDBUILD, s);
   return map_err(kd_build_records(d, n, bounds, s));
@@ -409,8 +458,11 @@ int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_phot
   if (st != PM_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_PTR_DEVICE(alloc_scope, a);
+  PM_PTR_DEVICE(alloc_scope, b);
   pm_photon_map* m = new pm_photon_map;
   m->made_on = s;
+  m->device = alloc_scope.dev;
   m->n = n;
   if (n > 0) {
     m->nodes.alloc(n);
@@ -447,6 +499,8 @@ int pm_photon_map_export(const pm_photon_map* m, pm_kd_photon* d_out, void* stre
   if (!m || (m->n > 0 && !d_out)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, m);
+  PM_PTR_DEVICE(alloc_scope, d_out);
   PM_TRY_ST(launch_map_export(m, d_out, s));
   return map_err(hipStreamSynchronize(s));
 }
@@ -455,7 +509,7 @@ int pm_photon_map_destroy(pm_photon_map* m) {
   if (m) {
     // back to the pool of the stream it was built on (a map built on a side
     // stream every frame would otherwise hipMalloc anew each time)
-    AllocStream pool(m->made_on);
+    AllocStream pool(m->made_on, m->device);
     delete m;
   }
   return PM_OK;
@@ -468,6 +522,8 @@ struct pm_kd_shard_plan {
   int64_t n = 0;
   int L = 0;   // 0: not split
   std::vector<int64_t> sizes;
+  hipStream_t made_on = nullptr;
+  int device = 0;
 };
 
 int pm_kd_shard_plan_create(const pm_photon* a, int64_t na, float pa, const pm_photon* b, int64_t nb, float pb,
@@ -480,7 +536,11 @@ int pm_kd_shard_plan_create(const pm_photon* a, int64_t na, float pa, const pm_p
   if (st != PM_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_PTR_DEVICE(alloc_scope, a);
+  PM_PTR_DEVICE(alloc_scope, b);
   pm_kd_shard_plan* p = new pm_kd_shard_plan;
+  p->made_on = s;
+  p->device = alloc_scope.dev;
   p->n = n;
   hipError_t e = hipSuccess;
   if (n > 0) {
@@ -529,6 +589,8 @@ int pm_kd_shard_build(pm_kd_shard_plan* p, int32_t j, int32_t* d_tags, void* str
   if (st != PM_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, p);
+  PM_PTR_DEVICE(alloc_scope, d_tags);
   reset_phase(PH_KDBUILD);
   hipError_t e;
   {
@@ -546,8 +608,11 @@ int pm_photon_map_create_sharded(pm_kd_shard_plan* p, const int32_t* subs, pm_ph
   if (st != PM_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, p);
+  PM_PTR_DEVICE(alloc_scope, subs);
   pm_photon_map* m = new pm_photon_map;
   m->made_on = s;
+  m->device = alloc_scope.dev;
   m->n = p->n;
   hipError_t e = hipSuccess;
   if (p->n > 0) {
@@ -577,7 +642,10 @@ int pm_photon_map_create_sharded(pm_kd_shard_plan* p, const int32_t* subs, pm_ph
 }
 
 int pm_kd_shard_plan_destroy(pm_kd_shard_plan* p) {
-  delete p;
+  if (p) {
+    AllocStream pool(p->made_on, p->device);
+    delete p;
+  }
   return PM_OK;
 }
 
@@ -586,6 +654,9 @@ int pm_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int32_t k, fl
   if (!m || nq < 0 || k < 1 || k > 256 || (nq > 0 && (!q || !ids)) || !(max_radius >= 0.f)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, m);
+  PM_PTR_DEVICE(alloc_scope, q);
+  PM_PTR_DEVICE(alloc_scope, ids);
   PM_TRY_ST(launch_knn(m, q, nq, k, max_radius, ids, d2, maxd2, s));
   return map_err(hipStreamSynchronize(s));
 }
@@ -595,6 +666,9 @@ int pm_gather(const pm_photon_map* m, const pm_float3* pts, const float* brdf, i
   if (!m || nq < 0 || (nq > 0 && (!pts || !brdf || !out))) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, m);
+  PM_PTR_DEVICE(alloc_scope, pts);
+  PM_PTR_DEVICE(alloc_scope, out);
   reset_phase(PH_GATHER);
   PhaseTimer tm(PH_GATHER, s);
   return map_err(launch_gather_api(m, pts, brdf, nq, out, s, kKNearest));
@@ -605,6 +679,9 @@ int pm_gather_k(const pm_photon_map* m, const pm_float3* pts, const float* brdf,
   if (!m || nq < 0 || k < 1 || k > 256 || (nq > 0 && (!pts || !brdf || !out))) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, m);
+  PM_PTR_DEVICE(alloc_scope, pts);
+  PM_PTR_DEVICE(alloc_scope, out);
   reset_phase(PH_GATHER);
   PhaseTimer tm(PH_GATHER, s);
   return map_err(launch_gather_api(m, pts, brdf, nq, out, s, k));
@@ -652,6 +729,7 @@ int pm_render_begin(pm_scene* sc, const pm_render_params* P, const pm_light* lig
   if (!render_params_ok(sc, P, lights, nl)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, sc);
   reset_phase(PH_PATHS);
   pm_render_job* J = render_job_new(sc, s);
   if (!J) return PM_ERR_OOM;
@@ -674,6 +752,8 @@ int pm_render_gather_caustic(pm_render_job* J, const pm_photon_map* cmap, void* 
   if (!J || !cmap || render_job_finished(J) || render_job_caustic_map(J)) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  if (render_job_device(J) != alloc_scope.dev) return PM_ERR_DEVICE;
+  PM_SAME_DEVICE(alloc_scope, cmap);
   reset_phase(PH_GATHER);
   {
     PhaseTimer tm(PH_GATHER, s);
@@ -689,6 +769,11 @@ int pm_render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_photo
   if (early ? (cmap && cmap != early) : !cmap) return PM_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  if (render_job_device(J) != alloc_scope.dev) return PM_ERR_DEVICE;
+  PM_SAME_DEVICE(alloc_scope, gmap);
+  PM_SAME_DEVICE(alloc_scope, cmap);
+  PM_PTR_DEVICE(alloc_scope, rgba);
+  PM_PTR_DEVICE(alloc_scope, rgb);
   reset_phase(PH_GATHER); reset_phase(PH_RESOLVE); reset_phase(PH_GATHER_GLOBAL);
   render_job_mark_finished(J);
   PM_TRY_ST(render_finish(J, gmap, cmap, rgba, rgb, s));
@@ -698,6 +783,27 @@ int pm_render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_photo
     g_render_stats = render_job_stats(J);
   }
   return check_overflow(render_job_scene(J), s);
+}
+
+int pm_render_job_queries(const pm_render_job* J, int32_t which, float* d_queries, float* d_results,
+                          int64_t capacity, int64_t* count, void* stream) {
+  if (!J || !count || (which != 0 && which != 1) || capacity < 0) return PM_ERR_INVALID;
+  const float4 *q = nullptr, *res = nullptr;
+  int64_t n = 0;
+  render_job_queries(J, which, &q, &res, &n);
+  *count = n;
+  if (!d_queries && !d_results) return PM_OK;   // size query
+  if (capacity < n) return PM_ERR_CAPACITY;
+  if (d_results && !render_job_finished(J)) return PM_ERR_INVALID;   // no results before finish
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  if (render_job_device(J) != alloc_scope.dev) return PM_ERR_DEVICE;
+  PM_PTR_DEVICE(alloc_scope, d_queries);
+  PM_PTR_DEVICE(alloc_scope, d_results);
+  if (n == 0) return PM_OK;
+  if (d_queries) PM_TRY_ST(hipMemcpyAsync(d_queries, q, sizeof(float4) * n, hipMemcpyDeviceToDevice, s));
+  if (d_results) PM_TRY_ST(hipMemcpyAsync(d_results, res, sizeof(float4) * n, hipMemcpyDeviceToDevice, s));
+  return map_err(hipStreamSynchronize(s));
 }
 
 int pm_render_job_destroy(pm_render_job* J) {
@@ -723,6 +829,9 @@ int pm_photon_view(pm_scene* sc, const pm_photon* d_photons, int64_t n, const pm
   if (int st = require_device()) return st;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, sc);
+  PM_PTR_DEVICE(alloc_scope, d_photons);
+  PM_PTR_DEVICE(alloc_scope, d_rgba);
   PM_TRY_ST(photon_view(sc, d_photons, n, *P, d_rgba, s));
   return check_overflow(sc, s);
 }
@@ -731,6 +840,7 @@ int pm_photons_quantize(pm_photon* d, int64_t n, void* stream) {
   if (n < 0 || (n > 0 && !d)) return PM_ERR_INVALID;
   if (int st = require_device()) return st;
   AllocStream alloc_scope((hipStream_t)stream);
+  PM_PTR_DEVICE(alloc_scope, d);
   return map_err(photons_quantize(d, n, (hipStream_t)stream));
 }
 

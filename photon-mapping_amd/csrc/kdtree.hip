@@ -340,10 +340,12 @@ __device__ __forceinline__ SegVal part_load(const KdLists& Lst, int64_t n, const
         c = kd_class(e[d], dim, nc, nid);
       } else {
         // count pass: the split coordinate alone decides unless it ties the
-        // median's (then the index does; the median itself has c == nc)
+        // median's (then the index does; the median itself has c == nc) --
+        // kd_class's predicate on the loaded coordinate (positions are never
+        // NaN: k_elems_* map NaN to +inf, so == and the sort keys agree)
         const float cv = Lst.comp(d, k, dim)[p];
         if (cv < nc) c = 0;
-        else if (cv > nc) c = 2;
+        else if (!(cv == nc)) c = 2;
         else {
           const int id = __float_as_int(Lst.comp(d, k, 3)[p]);
           c = id < nid ? 0 : (id == nid ? 1 : 2);
@@ -805,19 +807,26 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
 
 
 // ---------------------------------------------------------------- helpers for the C-ABI
+// A NaN coordinate becomes +inf (include/pm.h): the photon sorts last, compares
+// consistently in every pass (NaN compares false both ways, so the float
+// classification and the sort keys would disagree), and is never within a
+// gather radius.
+__device__ __forceinline__ float kd_coord(float x) { return x != x ? __int_as_float(0x7f800000) : x; }
+
 __global__ void k_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
                                      float pb, float4* elems, float4* payload) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= na + nb) return;
   const pm_photon p = i < na ? a[i] : b[i - na];
-  elems[i] = make_float4(p.pos.x, p.pos.y, p.pos.z, __int_as_float((int)i));
+  elems[i] = make_float4(kd_coord(p.pos.x), kd_coord(p.pos.y), kd_coord(p.pos.z), __int_as_float((int)i));
   payload[i] = make_float4(p.color.x, p.color.y, p.color.z, i < na ? pa : pb);
 }
 
 __global__ void k_elems_from_kd(const pm_kd_photon* in, int64_t n, float4* elems) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  elems[i] = make_float4(in[i].pos.x, in[i].pos.y, in[i].pos.z, __int_as_float((int)i));
+  elems[i] = make_float4(kd_coord(in[i].pos.x), kd_coord(in[i].pos.y), kd_coord(in[i].pos.z),
+                         __int_as_float((int)i));
 }
 
 __global__ void k_kd_reorder(const pm_kd_photon* src, const float4* nodes, int64_t n, pm_kd_photon* dst) {

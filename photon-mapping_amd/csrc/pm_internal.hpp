@@ -17,6 +17,7 @@ struct pm_scene {
   pmd::DevBuf<float4> mat;      // 2 per mesh
   pmd::DevBuf<int32_t> overflow;
   int32_t ntri = 0, nnodes = 0, nmesh = 0, depth = 0;
+  int device = 0;   // the HIP device its memory lives on (the creating thread's current device)
   pm_box bounds{};
   std::vector<pm_material> host_mat;
   pmd::DevScene view() const {
@@ -37,6 +38,7 @@ struct pm_photon_map {
   pmd::DevBuf<float4> payload;
   int64_t n = 0;
   hipStream_t made_on = nullptr;   // its memory returns to this stream's allocator pool
+  int device = 0;                  // the device of made_on
 };
 
 // PM_CHECK_VARIANT (build-time, tests only: lib_check/libpm_hip.so): every

@@ -8,36 +8,79 @@
 namespace pmd {
 
 // ------------------------------------------------------------ allocator
-// Free blocks are pooled per stream: a block returns to the pool of the stream
-// that is current (AllocStream) when it is freed, and is handed out again only
-// to work on that stream, so stream order makes reuse safe even when two host
-// threads drive two streams (pm_render_begin beside the photon trace). A block
-// that outlives an entry point is idle when freed (every entry point
-// synchronises its stream), so its pool does not matter.
+// Free blocks are pooled per (device, stream): a block returns to the pool of
+// the stream that is current (AllocStream) when it is freed, and is handed out
+// again only to work on that stream of its own device, so stream order makes
+// reuse safe even when two host threads drive two streams (pm_render_begin
+// beside the photon trace), and a block never crosses to another GPU when one
+// process drives several. A block that outlives an entry point is idle when
+// freed (every entry point synchronises its stream), so its pool does not
+// matter.
 namespace {
+struct PoolKey {
+  int dev;
+  hipStream_t s;
+  size_t sz;
+  bool operator<(const PoolKey& o) const {
+    if (dev != o.dev) return dev < o.dev;
+    if (s != o.s) return s < o.s;
+    return sz < o.sz;
+  }
+};
+struct Live {
+  size_t sz;
+  int dev;
+};
 std::mutex g_mu;
-std::multimap<std::pair<hipStream_t, size_t>, void*> g_free;   // (stream, size) -> block
-std::unordered_map<void*, size_t> g_live;                      // block -> size
+std::multimap<PoolKey, void*> g_free;    // (device, stream, size) -> block
+std::unordered_map<void*, Live> g_live;  // block -> (size, device)
 thread_local hipStream_t t_stream = nullptr;
 size_t round_up(size_t b) {
   size_t r = 256;
   while (r < b) r <<= 1;
   return r;
 }
+int current_device() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) {
+    (void)hipGetLastError();
+    d = 0;
+  }
+  return d;
+}
 }  // namespace
 
-AllocStream::AllocStream(hipStream_t s) : prev(t_stream) { t_stream = s; }
-AllocStream::~AllocStream() { t_stream = prev; }
+int stream_device(hipStream_t s) {
+  if (!s) return current_device();
+  hipDevice_t d = 0;
+  if (hipStreamGetDevice(s, &d) != hipSuccess) {
+    (void)hipGetLastError();
+    return current_device();
+  }
+  return (int)d;
+}
+
+AllocStream::AllocStream(hipStream_t s, int device) : prev(t_stream) {
+  const int cur = current_device();
+  dev = device >= 0 ? device : stream_device(s);
+  if (dev != cur && hipSetDevice(dev) == hipSuccess) restore = cur;
+  t_stream = s;
+}
+AllocStream::~AllocStream() {
+  t_stream = prev;
+  if (restore >= 0) (void)hipSetDevice(restore);
+}
 
 void* dev_alloc(size_t bytes) {
   const size_t sz = round_up(bytes ? bytes : 1);
+  const int dev = current_device();
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto it = g_free.find({t_stream, sz});
+    auto it = g_free.find(PoolKey{dev, t_stream, sz});
     if (it != g_free.end()) {
       void* p = it->second;
       g_free.erase(it);
-      g_live[p] = sz;
+      g_live[p] = Live{sz, dev};
       return p;
     }
   }
@@ -51,7 +94,7 @@ void* dev_alloc(size_t bytes) {
     }
   }
   std::lock_guard<std::mutex> lk(g_mu);
-  g_live[p] = sz;
+  g_live[p] = Live{sz, dev};
   return p;
 }
 
@@ -60,15 +103,52 @@ void dev_free(void* p) {
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_live.find(p);
   if (it == g_live.end()) return;
-  g_free.emplace(std::make_pair(t_stream, it->second), p);
+  g_free.emplace(PoolKey{it->second.dev, t_stream, it->second.sz}, p);
   g_live.erase(it);
 }
 
+// Releases the current device's idle blocks (after an out-of-memory).
 void dev_cache_trim() {
+  const int dev = current_device();
   (void)hipDeviceSynchronize();
   std::lock_guard<std::mutex> lk(g_mu);
-  for (auto& kv : g_free) (void)hipFree(kv.second);
-  g_free.clear();
+  for (auto it = g_free.begin(); it != g_free.end();) {
+    if (it->first.dev == dev) {
+      (void)hipFree(it->second);
+      it = g_free.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+
+void dev_pool_stats(int dev, size_t* live, size_t* cached) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  size_t l = 0, c = 0;
+  for (const auto& kv : g_live)
+    if (dev < 0 || kv.second.dev == dev) l += kv.second.sz;
+  for (const auto& kv : g_free)
+    if (dev < 0 || kv.first.dev == dev) c += kv.first.sz;
+  if (live) *live = l;
+  if (cached) *cached = c;
+}
+
+// One non-blocking side stream per device for the life of the process (the
+// render's caustic gather): its allocator pool then persists from frame to
+// frame (a per-job stream took its temporaries' pool with it).
+hipStream_t side_stream(int dev) {
+  static std::mutex mu;
+  static std::map<int, hipStream_t> streams;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  streams[dev] = s;
+  return s;
 }
 
 // ------------------------------------------------------------ scan

@@ -10,18 +10,30 @@
 namespace pmd {
 
 // Caching device allocator: freed blocks are kept and reused in stream order
-// (per-stream pools, see prims.hip), so timed loops do not hipMalloc.
+// (per-(device, stream) pools, see prims.hip), so timed loops do not hipMalloc.
+// Blocks come from the calling thread's current device.
 void* dev_alloc(size_t bytes);
-// Sets the calling thread's current stream for dev_alloc / dev_free (RAII; one
-// per entry point).
+// The device of a stream (the current device for the null stream).
+int stream_device(hipStream_t s);
+// One entry point's scope: makes `s`'s device (or `device` if >= 0) current
+// for the calling thread and `s` the stream of its dev_alloc / dev_free, and
+// restores both on exit (RAII). A host thread that never called hipSetDevice
+// is on device 0; this keeps every allocation and launch of a call on the
+// device of the stream it was given.
 struct AllocStream {
   hipStream_t prev;
-  explicit AllocStream(hipStream_t s);
+  int dev = 0;        // the call's device
+  int restore = -1;   // device to make current again on exit (-1: unchanged)
+  explicit AllocStream(hipStream_t s, int device = -1);
   ~AllocStream();
   AllocStream(const AllocStream&) = delete;
   AllocStream& operator=(const AllocStream&) = delete;
 };
 void dev_free(void* p);
+// Bytes held by live blocks and by idle pooled blocks of device `dev` (-1: all).
+void dev_pool_stats(int dev, size_t* live, size_t* cached);
+// The process-wide side stream of a device (created on first use).
+hipStream_t side_stream(int dev);
 void dev_cache_trim();
 
 template <typename T>

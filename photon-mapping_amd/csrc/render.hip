@@ -578,12 +578,9 @@ struct pm_render_job {
   pm_render_stats stats{};
   pm_scene* scene = nullptr;
   bool finished = false;
-  hipStream_t side = nullptr;   // the caustic gather's stream (render_finish), created on first use
   hipStream_t begun_on = nullptr;   // render_begin's stream: the job's buffers return to its allocator pool
+  int device = 0;                   // begun_on's device
   const pm_photon_map* caustic_map = nullptr;   // set once the caustic gather ran (render_gather_caustic)
-  ~pm_render_job() {
-    if (side) (void)hipStreamDestroy(side);
-  }
 };
 
 namespace pmd {
@@ -593,6 +590,7 @@ pm_render_job* render_job_new(pm_scene* sc, hipStream_t s) {
   if (J) {
     J->scene = sc;
     J->begun_on = s;
+    J->device = stream_device(s);
   }
   return J;
 }
@@ -602,11 +600,20 @@ pm_render_job* render_job_new(pm_scene* sc, hipStream_t s) {
 // back there (each begin a fresh hipMalloc, until memory runs out).
 void render_job_delete(pm_render_job* J) {
   if (!J) return;
-  AllocStream pool(J->begun_on);
+  AllocStream pool(J->begun_on, J->device);
   delete J;
 }
 const pm_render_stats& render_job_stats(const pm_render_job* J) { return J->stats; }
 pm_scene* render_job_scene(const pm_render_job* J) { return J->scene; }
+int render_job_device(const pm_render_job* J) { return J->device; }
+// The job's dense gather queries (pos, brdf) and results (radiance, 0) of one
+// map: which 0 = global (final gather), 1 = caustic.
+void render_job_queries(const pm_render_job* J, int which, const float4** q, const float4** res, int64_t* n) {
+  const pmd::SortedQueries& Q = which == 0 ? J->gs : J->cs;
+  *q = Q.n > 0 ? Q.dense : nullptr;
+  *res = Q.n > 0 ? (which == 0 ? J->gres.p : J->cres.p) : nullptr;
+  *n = Q.n;
+}
 bool render_job_finished(const pm_render_job* J) { return J->finished; }
 void render_job_mark_finished(pm_render_job* J) { J->finished = true; }
 const pm_photon_map* render_job_caustic_map(const pm_render_job* J) { return J->caustic_map; }
@@ -788,9 +795,12 @@ hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_p
     // synchronises its own stream before it returns.
     // (The global gather's own time comes from events read after the final
     // synchronisation: a host wait between the two would serialise them.)
+    // The side stream is the device's process-wide one, so the pool of the
+    // side gather's temporaries persists from frame to frame.
     PhaseTimer tm(PH_GATHER, s);
     const bool side = J->caustic_map == nullptr;
-    if (side && !J->side) PM_HIP_TRY(hipStreamCreateWithFlags(&J->side, hipStreamNonBlocking));
+    hipStream_t side_s = side ? side_stream(stream_device(s)) : nullptr;
+    if (side && !side_s) return hipErrorOutOfMemory;
     hipEvent_t ready = nullptr, done = nullptr, g0 = nullptr, g1 = nullptr;
     hipError_t e = hipEventCreate(&g0);
     if (e == hipSuccess) e = hipEventCreate(&g1);
@@ -798,23 +808,23 @@ hipError_t render_finish(pm_render_job* J, const pm_photon_map* gmap, const pm_p
       if (e == hipSuccess) e = hipEventCreateWithFlags(&ready, hipEventDisableTiming);
       if (e == hipSuccess) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
       if (e == hipSuccess) e = hipEventRecord(ready, s);
-      if (e == hipSuccess) e = hipStreamWaitEvent(J->side, ready, 0);
+      if (e == hipSuccess) e = hipStreamWaitEvent(side_s, ready, 0);
     }
     if (e == hipSuccess) e = hipEventRecord(g0, s);
     if (e == hipSuccess) e = gather_sorted(gmap, J->gs, J->gres.p, 1, s);
     if (e == hipSuccess) e = hipEventRecord(g1, s);
     if (side) {
       if (e == hipSuccess) {
-        AllocStream side_pool(J->side);   // the side gather's temporaries belong to its stream
-        e = gather_sorted(cmap, J->cs, J->cres.p, 0, J->side, J->A.caustic_k);
+        AllocStream side_pool(side_s);   // the side gather's temporaries belong to its stream
+        e = gather_sorted(cmap, J->cs, J->cres.p, 0, side_s, J->A.caustic_k);
       }
-      if (e == hipSuccess) e = hipEventRecord(done, J->side);
+      if (e == hipSuccess) e = hipEventRecord(done, side_s);
       if (e == hipSuccess) e = hipStreamWaitEvent(s, done, 0);
     }
     if (e == hipSuccess) e = hipEventSynchronize(g1);
     float ms = 0.f;
     if (e == hipSuccess && hipEventElapsedTime(&ms, g0, g1) == hipSuccess) record_phase_us(PH_GATHER_GLOBAL, ms * 1e3);
-    if (e != hipSuccess && side) (void)hipStreamSynchronize(J->side);   // no side work outlives a failed call
+    if (e != hipSuccess && side) (void)hipStreamSynchronize(side_s);   // no side work outlives a failed call
     for (hipEvent_t ev : {ready, done, g0, g1})
       if (ev) (void)hipEventDestroy(ev);
     PM_HIP_TRY(e);

@@ -30,7 +30,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PM_HIP_LIB", os.path.join(_HERE, "..", "lib", "libpm_hip.so"))
 
-PM_OK, PM_ERR_INVALID, PM_ERR_HIP, PM_ERR_OOM, PM_ERR_NO_DEVICE, PM_ERR_IO, PM_ERR_CAPACITY, PM_ERR_OVERFLOW = range(8)
+(PM_OK, PM_ERR_INVALID, PM_ERR_HIP, PM_ERR_OOM, PM_ERR_NO_DEVICE, PM_ERR_IO, PM_ERR_CAPACITY, PM_ERR_OVERFLOW,
+ PM_ERR_DEVICE) = range(9)
 PHASES = {"trace": 0, "compact": 1, "kdbuild": 2, "paths": 3, "gather": 4, "resolve": 5, "bvh": 6,
           "gather_global": 7}
 
@@ -142,6 +143,7 @@ _SIGNATURES = {
     "pm_device_free": (C.c_int, [_P]),
     "pm_copy_to_device": (C.c_int, [_P, _P, C.c_size_t]),
     "pm_copy_to_host": (C.c_int, [_P, _P, C.c_size_t]),
+    "pm_device_pool_stats": (C.c_int, [C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "pm_scene_create": (C.c_int, [C.POINTER(Mesh), C.c_int32, C.POINTER(_P)]),
     "pm_scene_stats_get": (C.c_int, [_P, C.POINTER(SceneStats)]),
     "pm_scene_destroy": (C.c_int, [_P]),
@@ -171,6 +173,7 @@ _SIGNATURES = {
     "pm_render_begin": (C.c_int, [_P, C.POINTER(RenderParams), C.POINTER(Light), C.c_int32, C.POINTER(_P), _P]),
     "pm_render_finish": (C.c_int, [_P, _P, _P, _P, _P, _P]),
     "pm_render_job_destroy": (C.c_int, [_P]),
+    "pm_render_job_queries": (C.c_int, [_P, C.c_int32, _P, _P, C.c_int64, C.POINTER(C.c_int64), _P]),
     "pm_render_gather_caustic": (C.c_int, [_P, _P, _P]),
     "pm_photon_view": (C.c_int, [_P, _P, C.c_int64, C.POINTER(ViewerParams), _P, _P]),
     "pm_config_load": (C.c_int, [C.c_char_p, C.POINTER(Config)]),
@@ -228,6 +231,13 @@ def device_count() -> int:
     n = C.c_int32(0)
     _lib.pm_device_count(C.byref(n))
     return n.value
+
+
+def pool_stats(device: int = -1):
+    """(live, cached) bytes of the library's caching allocator on `device` (-1: all)."""
+    live, cached = C.c_int64(0), C.c_int64(0)
+    _check(_lib.pm_device_pool_stats(int(device), C.byref(live), C.byref(cached)), "pm_device_pool_stats")
+    return live.value, cached.value
 
 
 def phase_us(name: str) -> float:
@@ -641,6 +651,20 @@ class RenderJob:
         _check(_lib.pm_render_finish(self._h, global_map.handle, caustic_map.handle if caustic_map else None,
                                      _ptr(rgba), _ptr(rgb), _stream(stream)), "pm_render_finish")
         return rgba, rgb
+
+    def queries(self, which: str = "global", results: bool = True, stream=None):
+        """pm_render_job_queries: (queries (n, 4) = hit point + brdf, results
+        (n, 4) = radiance + 0 or None) of the "global" or "caustic" gather,
+        in the job's dense order; results only after finish()."""
+        import torch
+        w = {"global": 0, "caustic": 1}[which]
+        n = C.c_int64(0)
+        _check(_lib.pm_render_job_queries(self._h, w, None, None, 0, C.byref(n), None), "pm_render_job_queries")
+        q = torch.empty((max(1, n.value), 4), dtype=torch.float32, device="cuda")
+        r = torch.empty((max(1, n.value), 4), dtype=torch.float32, device="cuda") if results else None
+        _check(_lib.pm_render_job_queries(self._h, w, _ptr(q), _ptr(r), q.shape[0], C.byref(n), _stream(stream)),
+               "pm_render_job_queries")
+        return q[: n.value], (r[: n.value] if r is not None else None)
 
     def close(self):
         if getattr(self, "_h", None):

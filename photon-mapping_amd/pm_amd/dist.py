@@ -304,9 +304,15 @@ class GpuBackend:
         if getattr(self, "_rside", None) is None:
             self._rside = torch.cuda.Stream()
         side, box = self._rside, {"c_ready": threading.Event()}
+        device = side.device   # this rank's GPU (the caller's current device)
 
         def run():
             try:
+                # HIP's and torch's current device are per host thread, and a new
+                # thread starts on device 0: without this, rank r's side thread
+                # would allocate its tensors (torch.empty(device="cuda")) on GPU 0
+                # (the library itself follows the stream's device, include/pm.h)
+                torch.cuda.set_device(device)
                 job = pm.render_begin(self.scene, self.cam, c.width, c.height, c.spp, c.depth, c.sky, self.lights,
                                       tile_rank=tile_rank, tile_count=tile_count, stream=side.cuda_stream,
                                       caustic_k=c.caustic_k)

@@ -10,7 +10,8 @@ to scratch). All of these are bit-identical by construction; the workloads of
 tests/variant_workloads.py run once per library (the check variant in ONE child
 process) and every output must match bit for bit. The full-size case is BASELINE
 config 3: 10M + 1M photons on the Sponza-class scene, the 45.4M-photon map and
-the 36M-query 1920x1080 final gather (seeded gather == plain walk at scale).
+the 36M-query 1920x1080 final gather (seeded gather == plain walk at scale),
+and config 5: 10M + 6.25M photons, the k = 200 caustic gather at 1920x1080.
 The spill path is also checked against the CPU oracle directly."""
 import os
 import subprocess
@@ -36,7 +37,7 @@ def runs(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("variant") / "check.npz")
     env = dict(os.environ, PM_HIP_LIB=VARIANT)
     r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "variant_workloads.py"), out, "--full"], env=env,
-                       capture_output=True, text=True, timeout=110)
+                       capture_output=True, text=True, timeout=115)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "lib_check/libpm_hip.so" in r.stdout, r.stdout
     prod = variant_workloads.run(full=True)
@@ -47,7 +48,8 @@ KEYS = ["cloud_hits", "cloud_occ", "cloud_photons", "cornell_g", "cornell_c", "c
         "gather_g", "gather_c", "gather_e", "knn_ids", "knn_d2", "knn_md", "render_64_rgba", "render_64_rgb",
         "render_64_stats", "render_40_rgba", "render_40_rgb", "render_40_stats", "kd_5", "kd_1023", "kd_1024",
         "kd_70000", "kd_2000003", "sphere_g", "sphere_c", "sphere_rgb", "sphere_stats"]
-FULL = ["c3_counts", "c3_g_crc", "c3_c_crc", "c3_gmap_crc", "c3_stats", "c3_rgba", "c3_rgb"]
+FULL = ["c3_counts", "c3_g_crc", "c3_c_crc", "c3_gmap_crc", "c3_stats", "c3_rgba", "c3_rgb",
+        "c5_counts", "c5_c_crc", "c5_cmap_crc", "c5_stats", "c5_rgba", "c5_rgb"]
 
 
 @pytest.mark.parametrize("key", KEYS + FULL)
@@ -60,6 +62,8 @@ def test_check_variant_bitwise(runs, key):
         assert a[3] > 30_000_000   # the full-size final gather: > 30M global-map queries
     if key == "c3_counts":
         assert a[0] > 40_000_000   # > 40M photons in the global map
+    if key == "c5_stats":
+        assert a[2] > 2_000_000    # the full-size k = 200 caustic gather: > 2M queries
 
 
 def test_spill_path_vs_oracle(runs):

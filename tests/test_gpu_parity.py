@@ -553,3 +553,47 @@ def test_render_caustic_k200_vs_oracle(cornell):
     k50 = _render_pair(meshes, lights, 20000, 48, 36, 1, caustic_k=50)[1]
     assert np.array_equal(_bits(ref), _bits(k50))
     assert not np.array_equal(_bits(ref), _bits(rgb))   # 200 neighbours change the caustic term
+
+
+def test_nan_positions_build_as_inf(cornell):
+    """a NaN photon coordinate compares false both ways, so the count
+    and partition passes of the kd build could classify it differently. Every
+    build takes NaN as +inf (include/pm.h): the map equals the oracle's map of
+    the same photons with NaN replaced by +inf, gathers and all, the sharded
+    build included, and in-place pm_kdtree_build keeps a valid tree."""
+    import oracle
+    import pm_amd
+    from pm_amd import dist as pmdist
+    meshes, lights = cornell
+    g = oracle.trace(oracle.Scene(meshes), lights, 20000, 10, False)
+    rng = np.random.default_rng(11)
+    bad = rng.choice(len(g), size=len(g) // 20, replace=False)
+    gn = g.copy()
+    gn[bad, rng.integers(0, 3, size=len(bad))] = np.nan
+    gi = gn.copy()
+    gi[:, 0:3] = np.where(np.isnan(gn[:, 0:3]), np.inf, gn[:, 0:3])
+    assert not np.isnan(gi[:, 0:3]).any() and np.isinf(gi[:, 0:3]).sum() == len(bad)
+    gm = pm_amd.PhotonMap(torch.from_numpy(gn).cuda(), 1.0)
+    om = oracle.PhotonMap(gi, 1.0)
+    q = (g[rng.integers(0, len(g), 1000), 0:3] + rng.normal(scale=0.5, size=(1000, 3))).astype(np.float32)
+    ids, d2, md = pm_amd.knn(gm, torch.from_numpy(q).cuda(), 50, 100.0)
+    oi, od, omd = om.knn(q, 50, 100.0)
+    assert np.array_equal(ids.cpu().numpy(), oi)
+    assert not np.isin(bad, ids.cpu().numpy()).any()
+    brdf = rng.uniform(0, 0.4, size=1000).astype(np.float32)
+    fg = pm_amd.gather_photons(gm, torch.from_numpy(q).cuda(), torch.from_numpy(brdf).cuda()).cpu().numpy()
+    assert np.array_equal(_bits(fg), _bits(om.gather(q, brdf)))
+    # the sharded build of the same photons: the same tree
+    t = torch.from_numpy(gn).cuda()
+    plan = pm_amd.KdShardPlan(t, 1.0, world=4)
+    if plan.sizes:
+        sm = pmdist.shard_assemble(plan, torch.cat([pmdist.shard_local(plan, r, 4)[0] for r in range(4)]), 4)
+        assert torch.equal(sm.export().view(torch.int32), gm.export().view(torch.int32))
+    # in place on kd records: a left-balanced tree over the +inf positions
+    rec = np.zeros((len(gn), 11), np.float32)
+    rec[:, 0:3] = gn[:, 0:3]
+    tr = torch.from_numpy(rec).cuda()
+    pm_amd.build_tree(tr, bounds=False)
+    out = tr.cpu().numpy()
+    pos = np.where(np.isnan(out[:, 0:3]), np.inf, out[:, 0:3])
+    _check_left_balanced(pos, (out[:, 10].view(np.uint32) >> 24).astype(np.int64))

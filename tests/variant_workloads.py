@@ -130,6 +130,20 @@ def run(full: bool = False) -> dict:
         rgba, rgb = pm_amd.render(sp, cam, 1920, 1080, 1, 30, (1, 1, 1), lights, gm, cm)
         out["c3_rgb"], out["c3_rgba"], out["c3_stats"] = rgb.cpu().numpy(), rgba.cpu().numpy(), _stats(pm_amd)
         out["c3_gmap_crc"] = _digest(gm.export())
+        del gm, cm, rgba, rgb, sp
+        # 6. config 5 at the bench's per-GPU size: 10 M + 6.25 M photons, square
+        # light + glass, the k = 200 caustic gather over the full caustic map
+        meshes, lights = scenes.sponza_caustics()
+        sp = pm_amd.Scene(meshes)
+        g = pm_amd.run_normal(sp, lights, 10_000_000, 10)
+        c = pm_amd.run_caustics(sp, lights, 6_250_000, 10)
+        out["c5_counts"] = np.array([g.shape[0], c.shape[0]], np.int64)
+        out["c5_c_crc"] = _digest(c)
+        gm, cm = pm_amd.load_photons(g, c)
+        del g, c
+        out["c5_cmap_crc"] = _digest(cm.export())
+        rgba, rgb = pm_amd.render(sp, cam, 1920, 1080, 1, 30, (1, 1, 1), lights, gm, cm, caustic_k=200)
+        out["c5_rgb"], out["c5_rgba"], out["c5_stats"] = rgb.cpu().numpy(), rgba.cpu().numpy(), _stats(pm_amd)
         del gm, cm, rgba, rgb
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
