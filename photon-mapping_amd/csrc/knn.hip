@@ -15,6 +15,7 @@
 // whenever any lane inserts: it is built from v_min_f64 / v_max_f64 only
 // (list_insert), and the walk tests a node's point post-order so root-path
 // points meet a tight bound (knn_walk, knn_walk_lean; variants measured: DESIGN.md §4.4).
+#include <algorithm>
 #include <cmath>
 
 #include "pm_internal.hpp"
@@ -666,11 +667,377 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
 #endif
 }
 
+// ---- wide gathers (k > 64; config 5: k = 200 caustic gather): collect and sort.
+// A K-wide sorted list in VGPRs stops paying above k ~ 64: every insert is a
+// 2K-op min/max network run by the whole wave, a 128-wide list holds the wave
+// at 2 waves/SIMD, and while a list fills under a loose cut-off nearly every
+// point the walk tests is inserted (the 128-wide pm_knn passes took ~120 ms for
+// config 5's 2.3 M caustic queries). Here a lane instead APPENDS each candidate
+// key (d^2 < its cut-off) to its own row of CAP = 64 S keys in global memory
+// (L2-resident: the rows of the waves in flight); when a row is full the wave
+// sorts it cooperatively (bitonic over 64 lanes x S keys, f64 min/max on the
+// gkey doubles), keeps the k smallest and tightens that lane's cut-off to the
+// k-th -- each flush handles CAP - k candidates. When the walks are over, each
+// row is sorted once more and its first min(cnt, k) keys are the exact k
+// nearest in (d^2, index) order; the lane sums gatherPhotons (shading.h:93-121)
+// over them in that order, exactly as radiance_g / k_radiance_k do.
+// Cut-offs: leaders (every kSeedStride-th walk rank) start from the plain
+// cut-off and record (position, k-th d^2); followers start from their leaders'
+// triangle-inequality bound (follower_cut holds for any k). A cut-off only
+// prunes: the kept keys are the k smallest either way.
+// The grid is persistent (rows per wave in flight): a wave takes groups of 64
+// consecutive walk ranks from an atomic counter until none are left.
+constexpr double kDblMax = 1.7976931348623157e308;   // pad key: above every gkey
+constexpr int kWideMinK = 64;                         // k > this: collect and sort
+
+__device__ __forceinline__ void fence_wave() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+// Bitonic sort (ascending) of 64 S keys held blocked: lane L holds elements
+// L S .. L S + S - 1. Strides >= S cross lanes (shuffles), smaller ones stay in
+// the lane's registers.
+template <int S>
+__device__ __forceinline__ void wave_sort(double (&v)[S], int lane) {
+  constexpr int N = 64 * S;
+#pragma unroll
+  for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+    for (int j = size >> 1; j > 0; j >>= 1) {
+      if (j >= S) {
+        const int lj = j / S;
+        const bool keep_min = (((lane * S) & size) == 0) == ((lane & lj) == 0);
+#pragma unroll
+        for (int r = 0; r < S; r++) {
+          const double p = __shfl_xor(v[r], lj);
+          v[r] = keep_min ? dmin(v[r], p) : dmax(v[r], p);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < S; r++) {
+          if (r & j) continue;
+          const bool up = (((lane * S + r) & size) == 0);
+          const double a = v[r], b = v[r | j];
+          const double mn = dmin(a, b), mx = dmax(a, b);
+          v[r] = up ? mn : mx;
+          v[r | j] = up ? mx : mn;
+        }
+      }
+    }
+  }
+}
+
+// Sort the first cnt (wave-uniform, <= 64 S) keys of a row, write its smallest
+// min(cnt, keep) back in order and return sorted[keep - 1] (meaningful when
+// cnt >= keep).
+template <int S>
+__device__ __forceinline__ double row_sort(double* __restrict__ row, int cnt, int keep, int lane) {
+  double v[S];
+#pragma unroll
+  for (int r = 0; r < S; r++) {
+    const int e = lane * S + r;
+    v[r] = e < cnt ? row[e] : kDblMax;
+  }
+  wave_sort<S>(v, lane);
+  const int m = cnt < keep ? cnt : keep;
+#pragma unroll
+  for (int r = 0; r < S; r++)
+    if (lane * S + r < m) row[lane * S + r] = v[r];
+  const int kt = keep - 1, kr = kt % S;
+  double t = v[0];
+#pragma unroll
+  for (int r = 1; r < S; r++) t = r == kr ? v[r] : t;
+  return __shfl(t, (kt / S) & 63);
+}
+
+// Subtree boxes (wide gathers): the AABB of every point in node c1's subtree,
+// box[2 (c1 - 1)] = (lo, _), box[2 (c1 - 1) + 1] = (hi, _), built bottom-up per
+// level for each wide gather call (k_subtree_box). The plane test alone cannot
+// prune a subtree whose splitting planes run past q while all of its points
+// are far away -- a dense caustic patch seen from a distant query, whose k
+// nearest lie in a thin shell across the patch -- so such walks visited nearly
+// every photon of the patch. A lane that arrives at a node from its parent
+// skips the subtree when the box's squared distance exceeds its bound. Exact:
+// per dimension the box gap is <= |q - p| for every point p inside, f32
+// subtraction, squaring and the (uncontracted) sum are monotone, so the box
+// distance computed in f32 is <= every inside point's computed d^2; a skipped
+// point has d^2 > bound, i.e. a key above the lane's tail.
+__global__ void k_subtree_box(const float4* __restrict__ nodes, int64_t n, int64_t lo, int64_t hi,
+                              float4* __restrict__ box) {
+  const int64_t t = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // 0-based node index
+  if (t >= hi) return;
+  const float4 p = nodes[t];
+  float4 a = make_float4(p.x, p.y, p.z, 0.f), b = a;
+#pragma unroll
+  for (int c = 1; c <= 2; c++) {
+    const int64_t ch = 2 * t + c;
+    if (ch < n) {
+      const float4 cl = box[2 * ch], ch_hi = box[2 * ch + 1];
+      a = make_float4(fminf(a.x, cl.x), fminf(a.y, cl.y), fminf(a.z, cl.z), 0.f);
+      b = make_float4(fmaxf(b.x, ch_hi.x), fmaxf(b.y, ch_hi.y), fmaxf(b.z, ch_hi.z), 0.f);
+    }
+  }
+  box[2 * t] = a;
+  box[2 * t + 1] = b;
+}
+
+static hipError_t build_subtree_boxes(const float4* nodes, int64_t n, float4* box, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  int D = 0;
+  while ((int64_t(2) << D) - 1 < n) D++;   // levels 0 .. D
+  for (int d = D; d >= 0; d--) {
+    const int64_t lo = (int64_t(1) << d) - 1, hi = std::min<int64_t>((int64_t(2) << d) - 1, n);
+    k_subtree_box<<<grid_for(hi - lo, 256), 256, 0, s>>>(nodes, n, lo, hi, box);
+    PM_HIP_TRY(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+#ifndef PM_WIDE_BOX
+#define PM_WIDE_BOX 1   // 0: plane test only (A/B variants)
+#endif
+__device__ __forceinline__ float box_d2(float4 a, float4 b, v3 q) {
+  const float gx = fmaxf(fmaxf(a.x - q.x, q.x - b.x), 0.f);
+  const float gy = fmaxf(fmaxf(a.y - q.y, q.y - b.y), 0.f);
+  const float gz = fmaxf(fmaxf(a.z - q.z, q.z - b.z), 0.f);
+  return gx * gx + gy * gy + gz * gz;
+}
+
+// One collect step of every lane: lean_step's walk and point test, the
+// candidate appended to the lane's row instead of an LDS insert queue, and a
+// subtree whose box lies beyond the bound skipped on arrival (`skip`: finished
+// at once, the walk leaves it as after its far child).
+template <bool WIDE>
+__device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, const float4* __restrict__ box,
+                                             uint32_t n, v3 q, double tail, LeanWalk& w, float4& nd, float4& ba,
+                                             float4& bb, double* __restrict__ row, int& cnt) {
+  const uint32_t word = __float_as_uint(nd.w);
+  const uint32_t dim = word & 3u;
+  const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
+  const float diff = dim == 0 ? dx : (dim == 1 ? dy : dz);
+  const bool skip = PM_WIDE_BOX && !w.up && box_d2(ba, bb, q) > w.bound;
+  const uint32_t close1 = 2 * w.c1 + (diff > 0.f ? 1u : 0u), far1 = close1 ^ 1u;
+  const bool closeok = close1 <= n;
+  const bool test = !skip && (w.up || !closeok);
+  const bool descend = !skip && !w.up && closeok;
+  const bool farok = !skip && !descend && far1 <= n && diff * diff <= w.bound;
+  const bool stay = descend || farok;
+  const uint32_t next = descend ? close1 : (farok ? far1 : w.upnode);
+  const bool go = w.walking && (stay || w.upnode != 0);
+  const uint32_t c1n = go ? next : w.c1;
+  const float4 ndn = node1<WIDE>(nodes, c1n);
+  const float4* bp = WIDE ? box + 2 * ((size_t)c1n - 1) : (const float4*)((const char*)box - 32 + (c1n << 5));
+  const float4 ban = bp[0], bbn = bp[1];
+  const float d2 = dx * dx + dy * dy + dz * dz;
+  const double key = gkey(d2, word);
+  const bool cand = w.walking && test && key < tail;
+  w.far_mask = stay ? (w.far_mask << 1 | (farok ? 1u : 0u)) : w.far_mask >> w.j1;
+  w.up = !stay;
+  if (cand) row[cnt] = key;
+  cnt += cand ? 1 : 0;
+  w.c1 = c1n;
+  w.walking = go;
+  w.set_jump();
+  nd = ndn;
+  ba = ban;
+  bb = bbn;
+}
+
+#ifndef PM_WIDE_STATS
+#define PM_WIDE_STATS 0
+#endif
+#if PM_WIDE_STATS
+// stats library only: [launch][0 groups, 1 iterations, 2 max iterations per group,
+// 3 flushes, 4 candidates, 5 valid lanes, 6 final keys]
+__device__ unsigned long long g_wide_stats[2][8];
+#endif
+
+template <int TAG, bool LEADERS, bool WIDE, int S>
+__global__ __launch_bounds__(256) void k_gather_wide(const float4* __restrict__ nodes,
+                                                     const float4* __restrict__ payload, int n,
+                                                     const float4* __restrict__ qb, int64_t nq,
+                                                     float4* __restrict__ out, const uint32_t* __restrict__ perm,
+                                                     float4* __restrict__ lead, int k, double* __restrict__ rows,
+                                                     uint32_t* __restrict__ counter, int64_t nitems,
+                                                     const float4* __restrict__ box) {
+  constexpr int CAP = 64 * S;
+  const float R2 = kKMaxDistance * kKMaxDistance;
+  const int lane = threadIdx.x & 63;
+  double* const wrows = rows + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * CAP;
+  double* const row = wrows + lane * CAP;
+  for (;;) {
+    uint32_t g = 0;
+    if (lane == 0) g = atomicAdd(counter, 1u);
+    g = __shfl(g, 0);
+    if ((int64_t)g * 64 >= nitems) break;   // wave-uniform: every wave reaches it
+    const int64_t t = (int64_t)g * 64 + lane;
+    const int64_t r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
+    const bool valid = t < nitems && r < nq;
+    const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
+    const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const v3 q = {qq.x, qq.y, qq.z};
+    float cut = lean_cut(R2);
+    if (valid && !LEADERS) cut = follower_cut(lead, nq, r, q, R2);
+    double tail = gkey(cut, kNoWord);
+    int cnt = 0;
+    if (n > 0) {
+      LeanWalk w;
+      w.start(cut, valid);
+      float4 nd = node1<WIDE>(nodes, 1), ba = box[0], bb = box[1];
+#if PM_WIDE_STATS
+      unsigned long long it = 0, fl = 0, nc = 0;
+#endif
+      for (;;) {
+#if PM_WIDE_STATS
+        const int c0 = cnt;
+#endif
+        collect_step<WIDE>(nodes, box, (uint32_t)n, q, tail, w, nd, ba, bb, row, cnt);
+        uint64_t full = ballot(cnt == CAP);
+#if PM_WIDE_STATS
+        it++;
+        fl += __popcll(full);
+        nc += cnt - c0;
+#endif
+        if (full) {   // flush: keep each full row's k smallest, tighten its cut-off
+          fence_wave();
+          while (full) {
+            const int l = __ffsll((long long)full) - 1;
+            full &= full - 1;
+            const double tl = row_sort<S>(wrows + l * CAP, CAP, k, lane);
+            if (lane == l) {
+              cnt = k;
+              tail = tl;
+              w.bound = gkey_d2(tl);
+            }
+          }
+          fence_wave();
+        }
+        if (ballot(w.walking) == 0) break;
+      }
+#if PM_WIDE_STATS
+      atomicAdd(&g_wide_stats[LEADERS][4], nc);
+      const uint64_t vm = ballot(valid);
+      if (lane == 0) {
+        atomicAdd(&g_wide_stats[LEADERS][0], 1ull);
+        atomicAdd(&g_wide_stats[LEADERS][1], it);
+        atomicMax(&g_wide_stats[LEADERS][2], it);
+        atomicAdd(&g_wide_stats[LEADERS][3], fl);
+        atomicAdd(&g_wide_stats[LEADERS][5], (unsigned long long)__popcll(vm));
+      }
+#endif
+    }
+#if PM_WIDE_STATS
+    atomicAdd(&g_wide_stats[LEADERS][6], (unsigned long long)cnt);
+#endif
+    // final sort of every row: its first min(cnt, k) keys in (d^2, index) order
+    fence_wave();
+#ifndef PM_WIDE_DIAG
+#define PM_WIDE_DIAG 0   // 1 (timing diagnostic only, wrong results): no final sorts
+#endif
+    uint64_t live = PM_WIDE_DIAG ? 0 : ballot(cnt > 0);
+    while (live) {
+      const int l = __ffsll((long long)live) - 1;
+      live &= live - 1;
+      const int cl = __shfl(cnt, l);
+      double* const rl = wrows + l * CAP;
+      if (cl <= 64) row_sort<1>(rl, cl, k, lane);
+      else if (cl <= 128) row_sort<2>(rl, cl, k, lane);
+      else if (S <= 4 || cl <= 256) row_sort<(S < 4 ? S : 4)>(rl, cl, k, lane);
+      else if (S <= 8 || cl <= 512) row_sort<(S < 8 ? S : 8)>(rl, cl, k, lane);
+      else row_sort<S>(rl, cl, k, lane);
+    }
+    fence_wave();
+    if (valid) {
+      const int m = cnt < k ? cnt : k;
+      const bool full = cnt >= k;
+      const float r2 = full ? gkey_d2(row[k - 1]) : R2;
+      v3 flux = {0.f, 0.f, 0.f};
+      for (int p = 0; p < m; p++) {
+        const double key = row[p];
+        const float4 pl = payload[gkey_word(key) >> 2];
+        const float dist = sqrtf(gkey_d2(key));
+        const float wgt = 1 - (dist / sqrtf(r2) * kConeFilterC);
+        flux = add(flux, smul(qq.w * pl.w * wgt, v3{pl.x, pl.y, pl.z}));
+      }
+      const v3 f = divf(flux, (1 - (2.f / 3.f) * (1.f / kConeFilterC)) * 2 * kPI * r2);
+      out[i] = make_float4(f.x, f.y, f.z, 0.f);
+      if (LEADERS) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, full ? r2 : -1.f);
+    }
+  }
+}
+
+static int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  return cus;
+}
+
+template <int S>
+static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out,
+                                       hipStream_t s, int k, const uint32_t* perm) {
+  constexpr int CAP = 64 * S;
+  const int n = (int)m->n;
+  const int64_t nl = (nq + kSeedStride - 1) / kSeedStride, nf = nq - nl;
+  const int64_t groups = (std::max(nl, nf) + 63) / 64;
+  // persistent grid: the workgroups the CUs hold at once, no more than there are groups
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_gather_wide<0, false, false, S>, 256, 0) !=
+          hipSuccess || per_cu <= 0)
+    per_cu = 4;
+  const int64_t wg = std::min<int64_t>((groups + 3) / 4, (int64_t)device_cus() * per_cu);
+  DevBuf<float4> lead(nl);
+  DevBuf<uint32_t> ctr(2);
+  DevBuf<double> rows((size_t)wg * 256 * CAP);
+  DevBuf<float4> box(2 * (size_t)std::max(n, 1));
+  if (!lead.p || !ctr.p || !rows.p || !box.p) return hipErrorOutOfMemory;
+  PM_HIP_TRY(hipMemsetAsync(ctr.p, 0, 2 * sizeof(uint32_t), s));
+  PM_HIP_TRY(build_subtree_boxes(m->nodes.p, n, box.p, s));
+#if PM_WIDE_STATS
+  {
+    static const unsigned long long zero[16] = {};
+    PM_HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wide_stats), zero, sizeof(zero), 0, hipMemcpyHostToDevice, s));
+  }
+#endif
+  const bool wide = n >= (1 << 28);
+#define PM_WIDE_LAUNCH(W)                                                                                          \
+  k_gather_wide<0, true, W, S><<<(int)std::min<int64_t>(wg, (nl + 255) / 256), 256, 0, s>>>(                     \
+      m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p, nl, box.p);                              \
+  PM_HIP_TRY(hipGetLastError());                                                                                 \
+  if (nf > 0) {                                                                                                  \
+    k_gather_wide<0, false, W, S><<<(int)std::min<int64_t>(wg, (nf + 255) / 256), 256, 0, s>>>(                  \
+        m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p + 1, nf, box.p);                        \
+    PM_HIP_TRY(hipGetLastError());                                                                               \
+  }
+  if (wide) {
+    PM_WIDE_LAUNCH(true)
+  } else {
+    PM_WIDE_LAUNCH(false)
+  }
+#undef PM_WIDE_LAUNCH
+#if PM_WIDE_STATS
+  {
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    unsigned long long st[2][8];
+    PM_HIP_TRY(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_wide_stats), sizeof(st)));
+    for (int L = 1; L >= 0; L--)
+      fprintf(stderr,
+              "[wide k=%d n=%d %s] groups %llu lanes %llu iters/group %.1f max %llu flushes/lane %.3f candidates/lane %.1f "
+              "final keys/lane %.1f\n",
+              k, n, L ? "leaders" : "followers", st[L][0], st[L][5], st[L][1] / (double)std::max(st[L][0], 1ull),
+              st[L][2], st[L][3] / (double)std::max(st[L][5], 1ull), st[L][4] / (double)std::max(st[L][5], 1ull),
+              st[L][6] / (double)std::max(st[L][5], 1ull));
+  }
+#endif
+  return hipStreamSynchronize(s);   // rows / leader records / boxes are freed on return
+}
+
 // ---- radiance estimate with k != 50 neighbours (k = 200
 // caustic gather). gatherPhotons (shading.h:93-121) over the k nearest: the
 // exact lists come from the pm_knn passes (k <= 128 one pass, up to 256 in
 // 128-wide passes), then one kernel sums them in (d^2, index) order with
 // r^2 = the k-th d^2 (max_radius^2 if fewer were found), as for k = 50.
+// Production runs k > 64 through the collect-and-sort gather above; the check
+// variant keeps these passes (independent code for the same lists).
 __global__ void k_q3_from_dense(const float4* __restrict__ qb, const uint32_t* __restrict__ perm, int64_t nq,
                                 pm_float3* __restrict__ q3) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -706,6 +1073,12 @@ hipError_t launch_gather_k(const pm_photon_map* m, const float4* qb, int64_t nq,
   if (nq <= 0) return hipSuccess;
   if (k < 1 || k > 256) return hipErrorInvalidValue;
   if (k == kKNearest) return launch_gather(m, qb, nq, out, s, 0, perm);
+#if !PM_CHECK_VARIANT
+  if (k > kWideMinK) {
+    if (k <= 200) return launch_gather_wide_s<8>(m, qb, nq, out, s, k, perm);
+    return launch_gather_wide_s<16>(m, qb, nq, out, s, k, perm);
+  }
+#endif
   DevBuf<pm_float3> q3(nq);
   DevBuf<int32_t> ids((size_t)nq * k);
   DevBuf<float> d2((size_t)nq * k), md(nq);
