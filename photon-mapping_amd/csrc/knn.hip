@@ -229,6 +229,106 @@ __device__ __forceinline__ float4 node1(const float4* __restrict__ nodes, uint32
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
+// Subtree boxes: the AABB of every point in node c1's subtree, box[2 (c1 - 1)]
+// = (lo, _), box[2 (c1 - 1) + 1] = (hi, _), for the nodes c1 <= nbox (the
+// levels down to a chosen depth), built per gather call (build_subtree_boxes).
+// The plane test alone cannot prune a subtree whose splitting planes run past q
+// while all of its points are far away -- a dense caustic patch seen from a
+// distant query, whose k nearest lie in a thin shell across the patch, or a
+// Cornell-box wall whose photons sit in a plane the query's close-path planes
+// cross -- so such walks visited nearly every photon there. A lane that
+// arrives at a boxed node from its parent skips the subtree when the box's
+// squared distance exceeds its bound. Exact: per dimension the box gap is
+// <= |q - p| for every point p inside, and f32 subtraction, squaring and the
+// (uncontracted) sum are monotone, so the box distance computed in f32 is <=
+// every inside point's computed d^2; a skipped point has d^2 > bound, i.e. a
+// key above the lane's tail.
+__global__ void k_subtree_box(const float4* __restrict__ nodes, int64_t n, int64_t lo, int64_t hi,
+                              float4* __restrict__ box) {
+  const int64_t t = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // 0-based node index
+  if (t >= hi) return;
+  const float4 p = nodes[t];
+  float4 a = make_float4(p.x, p.y, p.z, 0.f), b = a;
+#pragma unroll
+  for (int c = 1; c <= 2; c++) {
+    const int64_t ch = 2 * t + c;
+    if (ch < n) {
+      const float4 cl = box[2 * ch], chh = box[2 * ch + 1];
+      a = make_float4(fminf(a.x, cl.x), fminf(a.y, cl.y), fminf(a.z, cl.z), 0.f);
+      b = make_float4(fmaxf(b.x, chh.x), fmaxf(b.y, chh.y), fmaxf(b.z, chh.z), 0.f);
+    }
+  }
+  box[2 * t] = a;
+  box[2 * t + 1] = b;
+}
+// the deepest boxed level, from its points directly: node t's subtree holds
+// nodes (t + 1) 2^l - 1 + j, j < 2^l, at relative level l (contiguous per level)
+__global__ void k_subtree_box_scan(const float4* __restrict__ nodes, int64_t n, int64_t lo, int64_t hi, int levels,
+                                   float4* __restrict__ box) {
+  const int64_t t = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= hi) return;
+  float4 a = make_float4(INFINITY, INFINITY, INFINITY, 0.f), b = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+  for (int l = 0; l <= levels; l++) {
+    const int64_t f = ((t + 1) << l) - 1, e = std::min<int64_t>(((t + 2) << l) - 1, n);
+    for (int64_t j = f; j < e; j++) {
+      const float4 p = nodes[j];
+      a = make_float4(fminf(a.x, p.x), fminf(a.y, p.y), fminf(a.z, p.z), 0.f);
+      b = make_float4(fmaxf(b.x, p.x), fmaxf(b.y, p.y), fmaxf(b.z, p.z), 0.f);
+    }
+  }
+  box[2 * t] = a;
+  box[2 * t + 1] = b;
+}
+
+// Boxes of levels 0 .. D - skip (D = the deepest level; skip 0: every node).
+// Returns the number of boxed nodes (nbox) through *nbox.
+static hipError_t build_subtree_boxes(const float4* nodes, int64_t n, int skip, float4* box, int64_t* nbox,
+                                      hipStream_t s) {
+  *nbox = 0;
+  if (n <= 0) return hipSuccess;
+  int D = 0;
+  while ((int64_t(2) << D) - 1 < n) D++;   // levels 0 .. D (D may be partial)
+  int top = D;
+  if (skip > 0) {
+    top = std::max(D - skip, 0);   // a complete level (< D)
+    const int64_t lo = (int64_t(1) << top) - 1, hi = (int64_t(2) << top) - 1;
+    k_subtree_box_scan<<<grid_for(hi - lo, 256), 256, 0, s>>>(nodes, n, lo, hi, D - top, box);
+    PM_HIP_TRY(hipGetLastError());
+    top--;
+  }
+  for (int d = top; d >= 0; d--) {
+    const int64_t lo = (int64_t(1) << d) - 1, hi = std::min<int64_t>((int64_t(2) << d) - 1, n);
+    k_subtree_box<<<grid_for(hi - lo, 256), 256, 0, s>>>(nodes, n, lo, hi, box);
+    PM_HIP_TRY(hipGetLastError());
+  }
+  *nbox = skip > 0 ? (int64_t(2) << std::max(D - skip, 0)) - 1 : n;
+  return hipSuccess;
+}
+static int64_t boxed_nodes(int64_t n, int skip) {
+  if (n <= 0) return 0;
+  int D = 0;
+  while ((int64_t(2) << D) - 1 < n) D++;
+  return skip > 0 ? (int64_t(2) << std::max(D - skip, 0)) - 1 : n;
+}
+
+__device__ __forceinline__ float box_d2(float4 a, float4 b, v3 q) {
+  const float gx = fmaxf(fmaxf(a.x - q.x, q.x - b.x), 0.f);
+  const float gy = fmaxf(fmaxf(a.y - q.y, q.y - b.y), 0.f);
+  const float gz = fmaxf(fmaxf(a.z - q.z, q.z - b.z), 0.f);
+  return gx * gx + gy * gy + gz * gz;
+}
+// the boxes of node c1 (1-based, c1 <= nbox)
+template <bool WIDE>
+__device__ __forceinline__ const float4* box1(const float4* __restrict__ box, uint32_t c1) {
+  (void)WIDE;   // 32-B records: 64-bit offsets from 2^27 nodes on
+  return box + 2 * ((size_t)c1 - 1);
+}
+struct BoxView {
+  const float4* box = nullptr;
+  uint32_t nbox = 0;   // nodes 1 .. nbox carry a box
+};
+
+
 // One walk step of every lane (finished / idle lanes re-read their last node and
 // are masked): the post-order point test queues a candidate, the walk moves on.
 // Transitions (all computed, one selected):
@@ -236,9 +336,13 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_bal
 //  - else enter the far child if it exists and the plane is within the bound;
 //  - else JUMP to LeanWalk::upnode (arriving from its close child), or stop
 //    when that is 0.
-template <int K, bool WIDE>
+// BOX: a lane arriving at a boxed node from its parent skips the subtree when
+// its box lies beyond the bound (finished at once: the walk leaves it as after
+// its far child); ba / bb hold node c1's box (stale for unboxed nodes).
+template <int K, bool WIDE, bool BOX = false>
 __device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, uint32_t n, v3 q, double tail,
-                                          LeanWalk& w, float4& nd, double* lq, int lstride) {
+                                          LeanWalk& w, float4& nd, double* lq, int lstride, BoxView bx = {},
+                                          float4* ba = nullptr, float4* bb = nullptr) {
   // software-pipelined: `nd` (node c1) was loaded by the previous step; the
   // transitions come first, so the next node's load is issued before the point
   // test, the queue write and any insert round of this step
@@ -246,16 +350,22 @@ __device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, uint
   const uint32_t dim = word & 3u;
   const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
   const float diff = dim == 0 ? dx : (dim == 1 ? dy : dz);   // = q[dim] - nd[dim]
+  const bool skip = BOX && !w.up && w.c1 <= bx.nbox && box_d2(*ba, *bb, q) > w.bound;
   const uint32_t close1 = 2 * w.c1 + (diff > 0.f ? 1u : 0u), far1 = close1 ^ 1u;
   const bool closeok = close1 <= n;
-  const bool test = w.up || !closeok;
-  const bool descend = !w.up && closeok;
-  const bool farok = !descend && far1 <= n && diff * diff <= w.bound;
+  const bool test = !skip && (w.up || !closeok);
+  const bool descend = !skip && !w.up && closeok;
+  const bool farok = !skip && !descend && far1 <= n && diff * diff <= w.bound;
   const bool stay = descend || farok;
   const uint32_t next = descend ? close1 : (farok ? far1 : w.upnode);
   const bool go = w.walking && (stay || w.upnode != 0);
   const uint32_t c1n = go ? next : w.c1;
   const float4 ndn = node1<WIDE>(nodes, c1n);
+  if (BOX && c1n <= bx.nbox) {
+    const float4* bp = box1<WIDE>(bx.box, c1n);
+    *ba = bp[0];
+    *bb = bp[1];
+  }
   const float d2 = dx * dx + dy * dy + dz * dz;
   const double key = gkey(d2, word);
   const bool cand = w.walking && test && key < tail;
@@ -280,11 +390,39 @@ __device__ __forceinline__ void lean_round(double (&list)[K], LeanWalk& w, const
   w.bound = gkey_d2(list[K - 1]);
 }
 
-// BUDGET > 0: the walk stops after BUDGET wave iterations; lanes still walking
-// then are reported (return value) and their lists are incomplete.
-template <int K, int QL, bool WIDE, int BUDGET = 0>
+// One phase of the walk: steps (with or without subtree-box skips) until the
+// walks and queues are done (returns true) or the wave has run `limit`
+// iterations (false). BUDGET > 0: at BUDGET iterations the lanes still walking
+// stop and are reported through `aborted`; their lists are incomplete.
+template <int K, int QL, bool WIDE, int BUDGET, bool BOX>
+__device__ __forceinline__ bool lean_phase(const float4* __restrict__ nodes, uint32_t n, v3 q, double (&list)[K],
+                                           double* lq, int lstride, BoxView bx, LeanWalk& w, float4& nd, float4& ba,
+                                           float4& bb, int& it, int limit, bool& aborted) {
+  for (;;) {
+    lean_step<K, WIDE, BOX>(nodes, n, q, list[K - 1], w, nd, lq, lstride, bx, &ba, &bb);
+    ++it;
+    if (BUDGET > 0 && it == BUDGET) {
+      aborted = w.walking;
+      w.walking = false;
+    }
+    const bool any_walking = ballot(w.walking) != 0;
+    if (ballot(w.qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
+      lean_round<K>(list, w, lq, lstride);
+      if (!any_walking && ballot(w.qn > 0) == 0) return true;
+    }
+    if (it == limit) return false;
+  }
+}
+
+// BOXAFTER: < 0 plane tests only; >= 0 the walk switches to subtree-box skips
+// once the wave has run that many iterations (0: from the start). Box tests
+// cost ~14 VALU and a 32-B load per step, which the short walks of a dense map
+// do not pay back; the long ones -- a wave that wanders along planar walls or
+// a thin shell of a far patch -- are cut short by them.
+template <int K, int QL, bool WIDE, int BUDGET = 0, int BOXAFTER = -1>
 __device__ __forceinline__ bool knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float cut, bool valid,
-                                              double (&list)[K], double* lq, int lstride) {
+                                              double (&list)[K], double* lq, int lstride, BoxView bx = {},
+                                              int* it_out = nullptr) {
   const double sentinel = gkey(cut, kNoWord);
 #pragma unroll
   for (int j = 0; j < K; j++) list[j] = sentinel;
@@ -294,20 +432,23 @@ __device__ __forceinline__ bool knn_walk_lean(const float4* __restrict__ nodes, 
   w.qn = 0;
   lq[0] = __longlong_as_double(0x7FEFFFFFFFFFFFFFll);   // slot 0: DBL_MAX, never inserted
   float4 nd = node1<WIDE>(nodes, 1);
+  float4 ba = {}, bb = {};
   bool aborted = false;
   int it = 0;   // wave-uniform
-  for (;;) {
-    lean_step<K, WIDE>(nodes, (uint32_t)n, q, list[K - 1], w, nd, lq, lstride);
-    if (BUDGET > 0 && ++it == BUDGET) {
-      aborted = w.walking;
-      w.walking = false;
+  bool done = false;
+  if (BOXAFTER != 0)
+    done = lean_phase<K, QL, WIDE, BUDGET, false>(nodes, (uint32_t)n, q, list, lq, lstride, bx, w, nd, ba, bb, it,
+                                                  BOXAFTER, aborted);
+  if (BOXAFTER >= 0 && !done) {
+    if (w.c1 <= bx.nbox) {   // the current node's box (the skip test reads it next step)
+      const float4* bp = box1<WIDE>(bx.box, w.c1);
+      ba = bp[0];
+      bb = bp[1];
     }
-    const bool any_walking = ballot(w.walking) != 0;
-    if (ballot(w.qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
-      lean_round<K>(list, w, lq, lstride);
-      if (!any_walking && ballot(w.qn > 0) == 0) break;
-    }
+    lean_phase<K, QL, WIDE, BUDGET, true>(nodes, (uint32_t)n, q, list, lq, lstride, bx, w, nd, ba, bb, it, -1,
+                                          aborted);
   }
+  if (it_out) *it_out = it;
   return aborted;
 }
 
@@ -424,6 +565,35 @@ constexpr int kGatherQL = PM_GATHER_QL;   // LDS insert-queue depth
 #define PM_LEADER_BUDGET 2048
 #endif
 constexpr int kLeaderBudget = PM_LEADER_BUDGET;
+// Subtree-box skips in the k = 50 gather: 0 none, 1 leaders and retried
+// leaders, 2 every walk; boxes down to level D - PM_GATHER_BOX_SKIP (0: all).
+// Each walk switches to them after PM_BOX_AFTER wave iterations (knn_walk_lean).
+// Measured (round 3, ms per frame, config 2 / config 3): none 21.4 / 108.7;
+// every walk from the start 9.8 / 122.9 (config 3's global gather 41.6 ->
+// 55.8 ms: -24 % iterations but ~+14 VALU and a 32-B load per step); leaders
+// and retries only 15.9 / 111.0; boxes of the top levels only (skip 6) 10.5 /
+// 114.6; every walk after 256 / 512 / 1024 iterations 9.05 / 9.19 / 9.15 and
+// 111.7 / 108.8 / 108.5: 512 (config 2's global gather 16.3 -> 4.3 ms: the
+// long Cornell walks along the box walls end, config 3's walks mostly finish
+// before the switch).
+#ifndef PM_GATHER_BOX
+#define PM_GATHER_BOX 2
+#endif
+#ifndef PM_GATHER_BOX_SKIP
+#define PM_GATHER_BOX_SKIP 0
+#endif
+constexpr int kGatherBox = PM_GATHER_BOX;
+#ifndef PM_BOX_AFTER
+#define PM_BOX_AFTER 512
+#endif
+constexpr int kBoxAfter = PM_BOX_AFTER;
+#ifndef PM_KNN_STATS
+#define PM_KNN_STATS 0   // stats library only: walk iterations of the k = 50 gather
+#endif
+#if PM_KNN_STATS
+// [tag][leaders, followers, retry lanes][waves, iterations, max iterations]
+__device__ unsigned long long g_knn_stats[2][3][4];
+#endif
 
 __device__ __forceinline__ double seed_bound(float4 lead, v3 q) {
   if (!(lead.w >= 0.f)) return 1e300;
@@ -502,10 +672,10 @@ __device__ __forceinline__ float subtree_cut(const float4* __restrict__ nodes, u
 // kernel symbol (rocprof). perm: lane of walk rank r takes query perm[r] and
 // writes its result there (Morton walk order without permuted copies).
 template <int TAG, bool LEADERS, bool WIDE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_level(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && kGatherBox ? 3 : 4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
-    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks) {
+    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx) {
   __shared__ double lq[(kGatherQL + 1) * 256];
   const float R2 = kKMaxDistance * kKMaxDistance;
   // follower launch with a leader budget: the first nretry_blocks workgroups
@@ -532,8 +702,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   if (valid)
     cut = (LEADERS || redo_lane) ? subtree_cut<WIDE>(nodes, (uint32_t)n, q, cut) : follower_cut(lead, nq, r, q, R2);
   double list[kKNearest];
-  const bool aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0>(
-      nodes, n, q, cut, valid, list, lq + threadIdx.x, 256);
+  bool aborted;
+  int knn_it = 0;
+  int* const itp = PM_KNN_STATS ? &knn_it : nullptr;
+  if (kGatherBox == 2 || (kGatherBox == 1 && LEADERS)) {
+    aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0, kBoxAfter>(
+        nodes, n, q, cut, valid, list, lq + threadIdx.x, 256, bx, itp);
+  } else if (kGatherBox == 1 && redo_lane) {   // block-uniform: the retried leaders
+    aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, 0, kBoxAfter>(nodes, n, q, cut, valid, list,
+                                                                      lq + threadIdx.x, 256, bx, itp);
+  } else {
+    aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0>(nodes, n, q, cut, valid, list,
+                                                                                     lq + threadIdx.x, 256, {}, itp);
+  }
+#if PM_KNN_STATS
+  if ((threadIdx.x & 63) == 0) {
+    const int sl = LEADERS ? 0 : (redo_lane ? 2 : 1);
+    atomicAdd(&g_knn_stats[TAG][sl][0], 1ull);
+    atomicAdd(&g_knn_stats[TAG][sl][1], (unsigned long long)knn_it);
+    atomicMax(&g_knn_stats[TAG][sl][2], (unsigned long long)knn_it);
+  }
+#endif
   if (valid && !aborted) {
     const bool full = gkey_word(list[kKNearest - 1]) != kNoWord;
     const v3 f = radiance_g(list, payload, qq.w, full ? gkey_d2(list[kKNearest - 1]) : R2);
@@ -637,6 +826,15 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   DevBuf<uint32_t> retry(kLeaderBudget > 0 ? nl : 0), nretry(kLeaderBudget > 0 ? 1 : 0);
   if (!lead.p || (kLeaderBudget > 0 && (!retry.p || !nretry.p))) return hipErrorOutOfMemory;
   if (kLeaderBudget > 0) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, sizeof(uint32_t), s));
+  DevBuf<float4> box(kGatherBox ? 2 * (size_t)std::max<int64_t>(boxed_nodes(n, PM_GATHER_BOX_SKIP), 1) : 0);
+  BoxView bx;
+  if (kGatherBox) {
+    if (!box.p) return hipErrorOutOfMemory;
+    int64_t nbox = 0;
+    PM_HIP_TRY(build_subtree_boxes(m->nodes.p, n, PM_GATHER_BOX_SKIP, box.p, &nbox, s));
+    bx.box = box.p;
+    bx.nbox = (uint32_t)nbox;
+  }
   // followers (+ the retry workgroups first, with a leader budget)
   const int rb = kLeaderBudget > 0 ? grid_for(nl, 256) : 0;   // retry workgroups: one lane per leader
   const int gl = grid_for(nl, 256), gf = grid_for(nq - nl, 256) + rb;
@@ -644,11 +842,11 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   const bool wide = n >= (1 << 28);
 #define PM_LEVELS(T, W)                                                                                          \
   k_gather_level<T, true, W><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, retry.p, \
-                                                nretry.p, 0);                                                   \
+                                                nretry.p, 0, bx);                                               \
   PM_HIP_TRY(hipGetLastError());                                                                                \
   if (nq > nl || kLeaderBudget > 0)                                                                             \
   k_gather_level<T, false, W><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, retry.p, \
-                                                 nretry.p, rb)
+                                                 nretry.p, rb, bx)
   if (tag == 1) {
     if (wide) {
       PM_LEVELS(1, true);
@@ -663,6 +861,22 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
     }
   }
 #undef PM_LEVELS
+#if PM_KNN_STATS
+  {
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    unsigned long long st[2][3][4];
+    uint32_t nr = 0;
+    PM_HIP_TRY(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_knn_stats), sizeof(st)));
+    PM_HIP_TRY(hipMemcpy(&nr, nretry.p, sizeof(nr), hipMemcpyDeviceToHost));
+    const char* nm[3] = {"leaders", "followers", "retry"};
+    for (int j = 0; j < 3; j++)
+      fprintf(stderr, "[gather50 tag=%d n=%d nq=%lld %s] waves %llu iters/wave %.1f max %llu (retried leaders %u of %lld)\n",
+              tag, n, (long long)nq, nm[j], st[tag][j][0], st[tag][j][1] / (double)std::max(st[tag][j][0], 1ull),
+              st[tag][j][2], nr, (long long)nl);
+    static const unsigned long long zero[2][3][4] = {};
+    PM_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_knn_stats), zero, sizeof(zero)));
+  }
+#endif
   return hipGetLastError();
 #endif
 }
@@ -748,72 +962,25 @@ __device__ __forceinline__ double row_sort(double* __restrict__ row, int cnt, in
   return __shfl(t, (kt / S) & 63);
 }
 
-// Subtree boxes (wide gathers): the AABB of every point in node c1's subtree,
-// box[2 (c1 - 1)] = (lo, _), box[2 (c1 - 1) + 1] = (hi, _), built bottom-up per
-// level for each wide gather call (k_subtree_box). The plane test alone cannot
-// prune a subtree whose splitting planes run past q while all of its points
-// are far away -- a dense caustic patch seen from a distant query, whose k
-// nearest lie in a thin shell across the patch -- so such walks visited nearly
-// every photon of the patch. A lane that arrives at a node from its parent
-// skips the subtree when the box's squared distance exceeds its bound. Exact:
-// per dimension the box gap is <= |q - p| for every point p inside, f32
-// subtraction, squaring and the (uncontracted) sum are monotone, so the box
-// distance computed in f32 is <= every inside point's computed d^2; a skipped
-// point has d^2 > bound, i.e. a key above the lane's tail.
-__global__ void k_subtree_box(const float4* __restrict__ nodes, int64_t n, int64_t lo, int64_t hi,
-                              float4* __restrict__ box) {
-  const int64_t t = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // 0-based node index
-  if (t >= hi) return;
-  const float4 p = nodes[t];
-  float4 a = make_float4(p.x, p.y, p.z, 0.f), b = a;
-#pragma unroll
-  for (int c = 1; c <= 2; c++) {
-    const int64_t ch = 2 * t + c;
-    if (ch < n) {
-      const float4 cl = box[2 * ch], ch_hi = box[2 * ch + 1];
-      a = make_float4(fminf(a.x, cl.x), fminf(a.y, cl.y), fminf(a.z, cl.z), 0.f);
-      b = make_float4(fmaxf(b.x, ch_hi.x), fmaxf(b.y, ch_hi.y), fmaxf(b.z, ch_hi.z), 0.f);
-    }
-  }
-  box[2 * t] = a;
-  box[2 * t + 1] = b;
-}
-
-static hipError_t build_subtree_boxes(const float4* nodes, int64_t n, float4* box, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  int D = 0;
-  while ((int64_t(2) << D) - 1 < n) D++;   // levels 0 .. D
-  for (int d = D; d >= 0; d--) {
-    const int64_t lo = (int64_t(1) << d) - 1, hi = std::min<int64_t>((int64_t(2) << d) - 1, n);
-    k_subtree_box<<<grid_for(hi - lo, 256), 256, 0, s>>>(nodes, n, lo, hi, box);
-    PM_HIP_TRY(hipGetLastError());
-  }
-  return hipSuccess;
-}
-
 #ifndef PM_WIDE_BOX
 #define PM_WIDE_BOX 1   // 0: plane test only (A/B variants)
 #endif
-__device__ __forceinline__ float box_d2(float4 a, float4 b, v3 q) {
-  const float gx = fmaxf(fmaxf(a.x - q.x, q.x - b.x), 0.f);
-  const float gy = fmaxf(fmaxf(a.y - q.y, q.y - b.y), 0.f);
-  const float gz = fmaxf(fmaxf(a.z - q.z, q.z - b.z), 0.f);
-  return gx * gx + gy * gy + gz * gz;
-}
+#ifndef PM_WIDE_BOX_SKIP
+#define PM_WIDE_BOX_SKIP 0   // boxes down to level D - skip (0: every node)
+#endif
 
-// One collect step of every lane: lean_step's walk and point test, the
-// candidate appended to the lane's row instead of an LDS insert queue, and a
-// subtree whose box lies beyond the bound skipped on arrival (`skip`: finished
-// at once, the walk leaves it as after its far child).
+// One collect step of every lane: lean_step's walk and point test (with the
+// subtree-box skip), the candidate appended to the lane's row instead of an
+// LDS insert queue.
 template <bool WIDE>
-__device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, const float4* __restrict__ box,
-                                             uint32_t n, v3 q, double tail, LeanWalk& w, float4& nd, float4& ba,
-                                             float4& bb, double* __restrict__ row, int& cnt) {
+__device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, BoxView bx, uint32_t n, v3 q,
+                                             double tail, LeanWalk& w, float4& nd, float4& ba, float4& bb,
+                                             double* __restrict__ row, int& cnt) {
   const uint32_t word = __float_as_uint(nd.w);
   const uint32_t dim = word & 3u;
   const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
   const float diff = dim == 0 ? dx : (dim == 1 ? dy : dz);
-  const bool skip = PM_WIDE_BOX && !w.up && box_d2(ba, bb, q) > w.bound;
+  const bool skip = PM_WIDE_BOX && !w.up && w.c1 <= bx.nbox && box_d2(ba, bb, q) > w.bound;
   const uint32_t close1 = 2 * w.c1 + (diff > 0.f ? 1u : 0u), far1 = close1 ^ 1u;
   const bool closeok = close1 <= n;
   const bool test = !skip && (w.up || !closeok);
@@ -824,8 +991,11 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, c
   const bool go = w.walking && (stay || w.upnode != 0);
   const uint32_t c1n = go ? next : w.c1;
   const float4 ndn = node1<WIDE>(nodes, c1n);
-  const float4* bp = WIDE ? box + 2 * ((size_t)c1n - 1) : (const float4*)((const char*)box - 32 + (c1n << 5));
-  const float4 ban = bp[0], bbn = bp[1];
+  if (c1n <= bx.nbox) {
+    const float4* bp = box1<WIDE>(bx.box, c1n);
+    ba = bp[0];
+    bb = bp[1];
+  }
   const float d2 = dx * dx + dy * dy + dz * dz;
   const double key = gkey(d2, word);
   const bool cand = w.walking && test && key < tail;
@@ -837,8 +1007,6 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, c
   w.walking = go;
   w.set_jump();
   nd = ndn;
-  ba = ban;
-  bb = bbn;
 }
 
 #ifndef PM_WIDE_STATS
@@ -856,8 +1024,7 @@ __global__ __launch_bounds__(256) void k_gather_wide(const float4* __restrict__ 
                                                      const float4* __restrict__ qb, int64_t nq,
                                                      float4* __restrict__ out, const uint32_t* __restrict__ perm,
                                                      float4* __restrict__ lead, int k, double* __restrict__ rows,
-                                                     uint32_t* __restrict__ counter, int64_t nitems,
-                                                     const float4* __restrict__ box) {
+                                                     uint32_t* __restrict__ counter, int64_t nitems, BoxView bx) {
   constexpr int CAP = 64 * S;
   const float R2 = kKMaxDistance * kKMaxDistance;
   const int lane = threadIdx.x & 63;
@@ -881,7 +1048,7 @@ __global__ __launch_bounds__(256) void k_gather_wide(const float4* __restrict__ 
     if (n > 0) {
       LeanWalk w;
       w.start(cut, valid);
-      float4 nd = node1<WIDE>(nodes, 1), ba = box[0], bb = box[1];
+      float4 nd = node1<WIDE>(nodes, 1), ba = bx.box[0], bb = bx.box[1];
 #if PM_WIDE_STATS
       unsigned long long it = 0, fl = 0, nc = 0;
 #endif
@@ -889,7 +1056,7 @@ __global__ __launch_bounds__(256) void k_gather_wide(const float4* __restrict__ 
 #if PM_WIDE_STATS
         const int c0 = cnt;
 #endif
-        collect_step<WIDE>(nodes, box, (uint32_t)n, q, tail, w, nd, ba, bb, row, cnt);
+        collect_step<WIDE>(nodes, bx, (uint32_t)n, q, tail, w, nd, ba, bb, row, cnt);
         uint64_t full = ballot(cnt == CAP);
 #if PM_WIDE_STATS
         it++;
@@ -988,10 +1155,14 @@ static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb,
   DevBuf<float4> lead(nl);
   DevBuf<uint32_t> ctr(2);
   DevBuf<double> rows((size_t)wg * 256 * CAP);
-  DevBuf<float4> box(2 * (size_t)std::max(n, 1));
+  DevBuf<float4> box(2 * (size_t)std::max<int64_t>(boxed_nodes(n, PM_WIDE_BOX_SKIP), 1));
   if (!lead.p || !ctr.p || !rows.p || !box.p) return hipErrorOutOfMemory;
   PM_HIP_TRY(hipMemsetAsync(ctr.p, 0, 2 * sizeof(uint32_t), s));
-  PM_HIP_TRY(build_subtree_boxes(m->nodes.p, n, box.p, s));
+  int64_t nbox = 0;
+  PM_HIP_TRY(build_subtree_boxes(m->nodes.p, n, PM_WIDE_BOX_SKIP, box.p, &nbox, s));
+  BoxView bx;
+  bx.box = box.p;
+  bx.nbox = (uint32_t)nbox;
 #if PM_WIDE_STATS
   {
     static const unsigned long long zero[16] = {};
@@ -1001,11 +1172,11 @@ static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb,
   const bool wide = n >= (1 << 28);
 #define PM_WIDE_LAUNCH(W)                                                                                          \
   k_gather_wide<0, true, W, S><<<(int)std::min<int64_t>(wg, (nl + 255) / 256), 256, 0, s>>>(                     \
-      m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p, nl, box.p);                              \
+      m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p, nl, bx);                              \
   PM_HIP_TRY(hipGetLastError());                                                                                 \
   if (nf > 0) {                                                                                                  \
     k_gather_wide<0, false, W, S><<<(int)std::min<int64_t>(wg, (nf + 255) / 256), 256, 0, s>>>(                  \
-        m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p + 1, nf, box.p);                        \
+        m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p + 1, nf, bx);                        \
     PM_HIP_TRY(hipGetLastError());                                                                               \
   }
   if (wide) {

@@ -6,7 +6,10 @@ Makefile `budget`, built by __graft_entry__.build()): a leader wave stops after
 by the retry workgroups at the head of the follower launch (csrc/knn.hip,
 k_gather_level), while the followers fall back to whatever leaders finished
 (none: the plain cut-off). Production uses a budget of 2048 wave iterations,
-which mostly the Cornell box's wandering leader walks reach. The lists and radiance must not
+which mostly the Cornell box's wandering leader walks reach. The variant also
+switches every gather walk to subtree-box skips after one iteration
+(PM_BOX_AFTER=1; production: after 512, which these small workloads rarely
+reach), so the box path runs on all of them. The lists and radiance must not
 depend on either: the small workloads of tests/variant_workloads.py (seeded
 gathers with ties and duplicates, Cornell and sphere renders) run in one child
 process with the variant and must match production bit for bit."""

@@ -19,6 +19,8 @@ timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out
 tail -1 gpurun_out/bench.log
 timeout -k 10 300 python -u bench.py --config 2 --steps 10 --warmup 3 > gpurun_out/bench_c2.log 2>&1 || { echo BENCH_C2_FAILED; tail -20 gpurun_out/bench_c2.log; exit 6; }
 tail -1 gpurun_out/bench_c2.log
+timeout -k 10 300 python -u bench.py --config 5 --steps 5 --warmup 2 > gpurun_out/bench_c5.log 2>&1 || { echo BENCH_C5_FAILED; tail -20 gpurun_out/bench_c5.log; exit 7; }
+tail -1 gpurun_out/bench_c5.log
 cp gpurun_out/gpu_tests.log profiles/${TAG}_gpu_tests.log
 cp gpurun_out/bench.log profiles/${TAG}_bench.json.log
 cp gpurun_out/bench_c2.log profiles/${TAG}_bench_config2.json.log
