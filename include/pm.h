@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 3
+#define PM_ABI_VERSION 4
 
 enum pm_status {
   PM_OK = 0,
@@ -236,6 +236,34 @@ int pm_kd_shard_build(pm_kd_shard_plan* plan, int32_t subtree, int32_t* d_tags /
 int pm_photon_map_create_sharded(pm_kd_shard_plan* plan, const int32_t* d_tags,
                                  pm_photon_map** out, void* stream);
 int pm_kd_shard_plan_destroy(pm_kd_shard_plan* plan);
+
+/* Distributed top selection: the same top L levels and subtree sizes as
+ * pm_kd_shard_plan_create, computed from every rank's OWN photons before the
+ * exchange (each rank reads 1/G of the elements; no photon crosses ranks).
+ * d_a / d_b: this rank's photons of the two sets; a_first / b_first: the index
+ * of d_a[0] / d_b[0] in the gathered map (diffuse ++ caustic, rank order, so
+ * b_first = all ranks' diffuse count + the caustic count of lower ranks);
+ * n_total: the gathered map's size. Drive it with pm_kd_top_sel_step until
+ * *op == 0: each call consumes the reduction of the previous pass and issues
+ * the next into d_buf (int64, capacity PM_KD_TOP_SEL_BUF), whose first *count
+ * entries the caller reduces in place across all ranks -- *op 1: SUM, 2: MIN --
+ * before the next call (every rank runs the same number of steps). Then
+ * pm_kd_shard_plan_create_from_sel takes the gathered photons (as
+ * pm_kd_shard_plan_create would) and the rest is unchanged. A selection with
+ * no split (G == 1 or a small map) finishes at once and gives a plan with 0
+ * subtrees. */
+#define PM_KD_TOP_SEL_BUF 4096
+typedef struct pm_kd_top_sel pm_kd_top_sel;
+int pm_kd_top_sel_create(const pm_photon* d_a, int64_t na, int64_t a_first,
+                         const pm_photon* d_b, int64_t nb, int64_t b_first,
+                         int64_t n_total, int32_t world, pm_kd_top_sel** out, void* stream);
+int pm_kd_top_sel_step(pm_kd_top_sel* sel, int64_t* d_buf, int64_t* count, int32_t* op,
+                       void* stream);
+int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* sel,
+                                     const pm_photon* d_a, int64_t na, float power_a,
+                                     const pm_photon* d_b, int64_t nb, float power_b,
+                                     pm_kd_shard_plan** out, void* stream);
+int pm_kd_top_sel_destroy(pm_kd_top_sel* sel);
 
 /* ---- stage 2b: kNN + radiance estimate ----------------------------------
  * cukd::stackBased::knn<HeapCandidateList<k>> (shading.h:11-18): exact k

@@ -649,6 +649,132 @@ int pm_kd_shard_plan_destroy(pm_kd_shard_plan* p) {
   return PM_OK;
 }
 
+// ---- distributed top selection (kdshard.hip, KdTopSel)
+struct pm_kd_top_sel {
+  KdTopSel sel;
+  int64_t n_total = 0;
+  bool split = false;
+  hipStream_t made_on = nullptr;
+  int device = 0;
+};
+
+int pm_kd_top_sel_create(const pm_photon* a, int64_t na, int64_t a_first, const pm_photon* b, int64_t nb,
+                         int64_t b_first, int64_t n_total, int32_t world, pm_kd_top_sel** out, void* stream) {
+  if (!out || na < 0 || nb < 0 || a_first < 0 || b_first < 0 || world < 1 || (na > 0 && !a) || (nb > 0 && !b) ||
+      n_total < 0 || n_total >= kMaxMapPhotons || a_first + na > n_total || b_first + nb > n_total)
+    return PM_ERR_INVALID;
+  *out = nullptr;
+  int st = require_device();
+  if (st != PM_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  PM_PTR_DEVICE(alloc_scope, a);
+  PM_PTR_DEVICE(alloc_scope, b);
+  pm_kd_top_sel* h = new pm_kd_top_sel;
+  h->made_on = s;
+  h->device = alloc_scope.dev;
+  h->n_total = n_total;
+  const int L = shard_levels(world);
+  hipError_t e = hipSuccess;
+  if (world > 1 && shard_ok(n_total, L)) {
+    h->split = true;
+    reset_phase(PH_KDBUILD);
+    PhaseTimer tm(PH_KDBUILD, s);
+    e = h->sel.init(a, na, a_first, b, nb, b_first, n_total, L, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    delete h;
+    return map_err(e);
+  }
+  *out = h;
+  return PM_OK;
+}
+
+int pm_kd_top_sel_step(pm_kd_top_sel* h, int64_t* d_buf, int64_t* count, int32_t* op, void* stream) {
+  if (!h || !d_buf || !count || !op) return PM_ERR_INVALID;
+  *count = 0;
+  *op = 0;
+  if (!h->split) return PM_OK;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, h);
+  PM_PTR_DEVICE(alloc_scope, d_buf);
+  reset_phase(PH_KDBUILD);
+  int o = 0;
+  hipError_t e;
+  {
+    PhaseTimer tm(PH_KDBUILD, s);
+    e = h->sel.step(d_buf, count, &o, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  *op = o;
+  return map_err(e);
+}
+
+int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* h, const pm_photon* a, int64_t na, float pa,
+                                     const pm_photon* b, int64_t nb, float pb, pm_kd_shard_plan** out,
+                                     void* stream) {
+  if (!h || !out || na < 0 || nb < 0 || (na > 0 && !a) || (nb > 0 && !b) || na + nb != h->n_total ||
+      (h->split && h->sel.level < h->sel.L))
+    return PM_ERR_INVALID;   // the gathered map, after the last step
+  *out = nullptr;
+  int st = require_device();
+  if (st != PM_OK) return st;
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, h);
+  PM_PTR_DEVICE(alloc_scope, a);
+  PM_PTR_DEVICE(alloc_scope, b);
+  const int64_t n = na + nb;
+  pm_kd_shard_plan* p = new pm_kd_shard_plan;
+  p->made_on = s;
+  p->device = alloc_scope.dev;
+  p->n = n;
+  hipError_t e = hipSuccess;
+  if (n > 0) {
+    p->elems.alloc(n);
+    p->payload.alloc(n);
+    if (!p->elems.p || !p->payload.p) {
+      delete p;
+      return PM_ERR_OOM;
+    }
+    reset_phase(PH_KDBUILD);
+    PhaseTimer tm(PH_KDBUILD, s);
+    e = launch_elems_from_photons(a, na, b, nb, pa, pb, p->elems.p, p->payload.p, s);
+    if (e == hipSuccess && h->split) {
+      const int L = h->sel.L;
+      p->top.alloc((size_t)1 << L);
+      if (!p->top.p) e = hipErrorOutOfMemory;
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(p->top.p, h->sel.top.p, sizeof(float4) * (((size_t)1 << L) - 1), hipMemcpyDeviceToDevice,
+                           s);
+      if (e == hipSuccess) e = kd_shard_top_fix(p->elems.p, p->top.p, L, s);
+      if (e == hipSuccess) {
+        p->sizes = h->sel.seg;
+        p->sub.alloc(n);
+        e = p->sub.p ? kd_shard_classify(p->elems.p, n, L, p->top.p, p->sub.p, s) : hipErrorOutOfMemory;
+      }
+      if (e == hipSuccess) p->L = L;
+    }
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    delete p;
+    return map_err(e);
+  }
+  *out = p;
+  return PM_OK;
+}
+
+int pm_kd_top_sel_destroy(pm_kd_top_sel* h) {
+  if (h) {
+    AllocStream pool(h->made_on, h->device);
+    delete h;
+  }
+  return PM_OK;
+}
+
 int pm_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int32_t k, float max_radius, int32_t* ids,
            float* d2, float* maxd2, void* stream) {
   if (!m || nq < 0 || k < 1 || k > 256 || (nq > 0 && (!q || !ids)) || !(max_radius >= 0.f)) return PM_ERR_INVALID;

@@ -17,7 +17,10 @@
 // Deviation: the reference rewrites '/' to '\\' before
 // opening lights.txt / .mtl and so cannot load a scene on Linux; both
 // separators are accepted here.
+#include <algorithm>
+#include <array>
 #include <cmath>
+#include <functional>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -30,6 +33,8 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+
+#include <zlib.h>
 
 #include "../../../include/pm.h"
 
@@ -433,6 +438,348 @@ bool load_obj(const std::string& path, RawScene& sc, std::string& err) {
   return true;
 }
 
+// ------------------------------------------------------------------ FBX
+// Binary FBX (7100-7500; the reference's assets/models/cornell-box/cornell-box.fbx
+// is 7400, reached through assimp at assetImporter.cxx:18-21). What assimp's
+// FBX importer (+ Triangulate) hands extract_objects, restated:
+//   * nodes: a root over the models connected to object 0 (connection order),
+//     each model's children likewise; the model matrix is T * R * S in float
+//     (aiMatrix4x4 products), R = Rz * Ry * Rx of the Euler angles in degrees
+//     (rotation order XYZ). Pivots, offsets, pre/post and geometric transforms
+//     would make assimp insert helper nodes: rejected here (none in the assets);
+//   * meshes: one per (geometry, material index) in first-appearance order,
+//     vertices = polygon corners (positions cast from double), named after the
+//     model's connected material ("DefaultMaterial" when none);
+//   * Triangulate: quads split from the first vertex whose two angles to the
+//     diagonal exceed pi (assimp's concave-quad rule), larger polygons as a fan.
+// Parity for FBX is unpinned: assimp cannot be run here; tests compare the
+// scene against the same model's GLB.
+struct FbxProp {
+  char type = 0;
+  double num = 0.0;      // scalar types
+  int64_t inum = 0;
+  std::string str;       // S / R
+  std::vector<double> darr;   // f / d arrays
+  std::vector<int64_t> iarr;  // i / l / b arrays
+};
+struct FbxNode {
+  std::string name;
+  std::vector<FbxProp> props;
+  std::vector<FbxNode> kids;
+  const FbxNode* child(const char* n) const {
+    for (const FbxNode& k : kids)
+      if (k.name == n) return &k;
+    return nullptr;
+  }
+};
+
+struct FbxReader {
+  const std::string& b;
+  bool wide = false;
+  std::string err;
+  template <typename T>
+  bool rd(size_t o, T& v) {
+    if (o + sizeof(T) > b.size()) return false;
+    std::memcpy(&v, b.data() + o, sizeof(T));
+    return true;
+  }
+  bool array(size_t& p, char t, FbxProp& pr) {
+    uint32_t n = 0, enc = 0, clen = 0;
+    if (!rd(p, n) || !rd(p + 4, enc) || !rd(p + 8, clen) || p + 12 + (size_t)clen > b.size()) return false;
+    p += 12;
+    const size_t es = (t == 'd' || t == 'l') ? 8 : (t == 'b' ? 1 : 4);
+    std::string raw;
+    if (enc == 0) {
+      if ((size_t)n * es != clen) return false;
+      raw.assign(b.data() + p, clen);
+    } else if (enc == 1) {
+      raw.resize((size_t)n * es);
+      uLongf dl = (uLongf)raw.size();
+      if (uncompress((Bytef*)&raw[0], &dl, (const Bytef*)b.data() + p, clen) != Z_OK || dl != raw.size()) return false;
+    } else {
+      return false;
+    }
+    p += clen;
+    for (uint32_t i = 0; i < n; i++) {
+      const char* q = raw.data() + (size_t)i * es;
+      if (t == 'd') { double v; std::memcpy(&v, q, 8); pr.darr.push_back(v); }
+      else if (t == 'f') { float v; std::memcpy(&v, q, 4); pr.darr.push_back(v); }
+      else if (t == 'l') { int64_t v; std::memcpy(&v, q, 8); pr.iarr.push_back(v); }
+      else if (t == 'i') { int32_t v; std::memcpy(&v, q, 4); pr.iarr.push_back(v); }
+      else pr.iarr.push_back(*q ? 1 : 0);
+    }
+    return true;
+  }
+  // one node record at o; false on a malformed record; `null` for the end marker
+  bool node(size_t& o, FbxNode& out, bool& null, int depth) {
+    uint64_t end = 0, nprop = 0, plen = 0;
+    if (wide) {
+      if (!rd(o, end) || !rd(o + 8, nprop) || !rd(o + 16, plen)) return false;
+      o += 24;
+    } else {
+      uint32_t e32, n32, p32;
+      if (!rd(o, e32) || !rd(o + 4, n32) || !rd(o + 8, p32)) return false;
+      end = e32, nprop = n32, plen = p32;
+      o += 12;
+    }
+    uint8_t nl = 0;
+    if (!rd(o, nl)) return false;
+    o += 1;
+    null = end == 0;
+    if (null) return true;
+    if (end > b.size() || o + nl > end || depth > 64) return false;
+    out.name.assign(b.data() + o, nl);
+    o += nl;
+    size_t p = o;
+    for (uint64_t k = 0; k < nprop; k++) {
+      FbxProp pr;
+      if (p >= end) return false;
+      pr.type = b[p++];
+      switch (pr.type) {
+        case 'Y': { int16_t v; if (!rd(p, v)) return false; pr.inum = v; pr.num = v; p += 2; break; }
+        case 'C': { uint8_t v; if (!rd(p, v)) return false; pr.inum = v; pr.num = v; p += 1; break; }
+        case 'I': { int32_t v; if (!rd(p, v)) return false; pr.inum = v; pr.num = v; p += 4; break; }
+        case 'F': { float v; if (!rd(p, v)) return false; pr.num = v; pr.inum = (int64_t)v; p += 4; break; }
+        case 'D': { double v; if (!rd(p, v)) return false; pr.num = v; pr.inum = (int64_t)v; p += 8; break; }
+        case 'L': { int64_t v; if (!rd(p, v)) return false; pr.inum = v; pr.num = (double)v; p += 8; break; }
+        case 'f': case 'd': case 'l': case 'i': case 'b':
+          if (!array(p, pr.type, pr)) return false;
+          break;
+        case 'S': case 'R': {
+          uint32_t n; if (!rd(p, n) || p + 4 + (size_t)n > end) return false;
+          pr.str.assign(b.data() + p + 4, n);
+          p += 4 + n;
+          break;
+        }
+        default:
+          return false;
+      }
+      out.props.push_back(std::move(pr));
+    }
+    o = p;
+    while (o < end) {
+      FbxNode kid;
+      bool kn = false;
+      if (!node(o, kid, kn, depth + 1)) return false;
+      if (kn) break;
+      out.kids.push_back(std::move(kid));
+    }
+    o = (size_t)end;
+    return true;
+  }
+};
+
+// "name\0\1Class" -> name
+std::string fbx_name(const std::string& s) {
+  const size_t z = s.find('\0');
+  return z == std::string::npos ? s : s.substr(0, z);
+}
+
+// Properties70 P records of a model: name -> values (doubles)
+std::map<std::string, std::vector<double>> fbx_p70(const FbxNode& obj) {
+  std::map<std::string, std::vector<double>> out;
+  const FbxNode* p70 = obj.child("Properties70");
+  if (!p70) return out;
+  for (const FbxNode& p : p70->kids) {
+    if (p.name != "P" || p.props.empty()) continue;
+    std::vector<double> v;
+    for (size_t i = 4; i < p.props.size(); i++) v.push_back(p.props[i].num);
+    out[p.props[0].str] = v;
+  }
+  return out;
+}
+
+// aiMatrix4x4::RotationX / Y / Z (angle in radians, float)
+Mat4 rot_axis(int axis, float a) {
+  Mat4 R = Mat4::identity();
+  const float c = std::cos(a), s = std::sin(a);
+  const int i = (axis + 1) % 3, j = (axis + 2) % 3;
+  R.m[i][i] = c;
+  R.m[i][j] = -s;
+  R.m[j][i] = s;
+  R.m[j][j] = c;
+  return R;
+}
+
+bool load_fbx(const std::string& path, RawScene& sc, std::string& err) {
+  std::string b;
+  if (!read_file(path, b)) { err = "cannot open " + path; return false; }
+  static const char magic[] = "Kaydara FBX Binary  ";
+  if (b.size() < 27 || std::memcmp(b.data(), magic, 20) != 0) {
+    err = "not a binary FBX (ASCII FBX is not supported)";
+    return false;
+  }
+  uint32_t ver = 0;
+  std::memcpy(&ver, b.data() + 23, 4);
+  FbxReader R{b};
+  R.wide = ver >= 7500;
+  std::vector<FbxNode> top;
+  size_t o = 27;
+  while (o < b.size()) {
+    FbxNode nd;
+    bool null = false;
+    if (!R.node(o, nd, null, 0)) { err = "malformed FBX record"; return false; }
+    if (null) break;
+    top.push_back(std::move(nd));
+  }
+  const FbxNode* objects = nullptr;
+  const FbxNode* conns = nullptr;
+  for (const FbxNode& n : top) {
+    if (n.name == "Objects") objects = &n;
+    if (n.name == "Connections") conns = &n;
+  }
+  if (!objects || !conns) { err = "FBX without Objects / Connections"; return false; }
+  std::map<int64_t, const FbxNode*> geoms, models, mats;
+  for (const FbxNode& ob : objects->kids) {
+    if (ob.props.empty()) continue;
+    const int64_t id = ob.props[0].inum;
+    if (ob.name == "Geometry" && ob.props.size() >= 3 && ob.props[2].str == "Mesh") geoms[id] = &ob;
+    else if (ob.name == "Model") models[id] = &ob;
+    else if (ob.name == "Material") mats[id] = &ob;
+  }
+  // object-object connections in file order: child -> parent
+  std::vector<std::pair<int64_t, int64_t>> oo;
+  for (const FbxNode& c : conns->kids)
+    if (c.name == "C" && c.props.size() >= 3 && c.props[0].str == "OO") oo.push_back({c.props[1].inum, c.props[2].inum});
+  // model -> its geometries / materials / child models, in connection order
+  std::map<int64_t, std::vector<int64_t>> mgeo, mmat, mkids;
+  std::vector<int64_t> roots;
+  for (const auto& [ch, par] : oo) {
+    if (geoms.count(ch) && models.count(par)) mgeo[par].push_back(ch);
+    else if (mats.count(ch) && models.count(par)) mmat[par].push_back(ch);
+    else if (models.count(ch)) {
+      if (par == 0) roots.push_back(ch);
+      else if (models.count(par)) mkids[par].push_back(ch);
+    }
+  }
+  static const char* complex[] = {"RotationOffset", "RotationPivot", "PreRotation", "PostRotation", "ScalingOffset",
+                                  "ScalingPivot", "GeometricTranslation", "GeometricRotation", "GeometricScaling"};
+  std::map<int64_t, int> node_of;
+  std::function<int(int64_t)> build_node = [&](int64_t id) -> int {
+    const FbxNode& m = *models.at(id);
+    const auto P = fbx_p70(m);
+    for (const char* c : complex) {
+      auto it = P.find(c);
+      if (it == P.end()) continue;
+      const double idv = std::string(c).find("Scaling") != std::string::npos && std::string(c).find("Geometric") == 0
+                             ? 1.0 : 0.0;
+      for (double v : it->second)
+        if (v != idv) { err = std::string("FBX transform component not supported: ") + c; return -1; }
+    }
+    auto ro = P.find("RotationOrder");
+    if (ro != P.end() && !ro->second.empty() && ro->second[0] != 0.0) { err = "FBX rotation order not XYZ"; return -1; }
+    RawNode nd;
+    nd.M = Mat4::identity();
+    auto vec = [&](const char* k, float d) {
+      auto it = P.find(k);
+      std::array<float, 3> v{d, d, d};
+      if (it != P.end() && it->second.size() >= 3)
+        for (int i = 0; i < 3; i++) v[i] = (float)it->second[i];
+      return v;
+    };
+    const auto t = vec("Lcl Translation", 0.f), r = vec("Lcl Rotation", 0.f), s = vec("Lcl Scaling", 1.f);
+    Mat4 T = Mat4::identity();
+    T.m[0][3] = t[0], T.m[1][3] = t[1], T.m[2][3] = t[2];
+    const float d2r = (float)(3.14159265358979323846 / 180.0);
+    Mat4 Rm = Mat4::identity();
+    if (r[0] != 0.f || r[1] != 0.f || r[2] != 0.f)
+      Rm = mul(mul(rot_axis(2, r[2] * d2r), rot_axis(1, r[1] * d2r)), rot_axis(0, r[0] * d2r));
+    Mat4 S = Mat4::identity();
+    S.m[0][0] = s[0], S.m[1][1] = s[1], S.m[2][2] = s[2];
+    nd.M = mul(mul(mul(nd.M, T), Rm), S);
+    // meshes: per geometry, per material index in first-appearance order
+    for (int64_t gid : mgeo[id]) {
+      const FbxNode& g = *geoms.at(gid);
+      const FbxNode* vn = g.child("Vertices");
+      const FbxNode* pn = g.child("PolygonVertexIndex");
+      if (!vn || !pn || vn->props.empty() || pn->props.empty()) { err = "FBX mesh without vertices"; return -1; }
+      const std::vector<double>& V = vn->props[0].darr;
+      const std::vector<int64_t>& PI = pn->props[0].iarr;
+      std::vector<std::vector<int>> polys;
+      std::vector<int> cur;
+      for (int64_t x : PI) {
+        const int64_t v = x < 0 ? ~x : x;
+        if (v < 0 || 3 * v + 2 >= (int64_t)V.size()) { err = "FBX polygon index out of range"; return -1; }
+        cur.push_back((int)v);
+        if (x < 0) {
+          polys.push_back(cur);
+          cur.clear();
+        }
+      }
+      std::vector<int> pmat(polys.size(), 0);
+      if (const FbxNode* lm = g.child("LayerElementMaterial")) {
+        const FbxNode* mp = lm->child("MappingInformationType");
+        const FbxNode* mi = lm->child("Materials");
+        if (mp && mi && !mp->props.empty() && !mi->props.empty()) {
+          const auto& idx = mi->props[0].iarr;
+          if (mp->props[0].str == "ByPolygon") {
+            for (size_t k = 0; k < polys.size() && k < idx.size(); k++) pmat[k] = (int)idx[k];
+          } else if (!idx.empty()) {
+            std::fill(pmat.begin(), pmat.end(), (int)idx[0]);
+          }
+        }
+      }
+      std::vector<int> order;
+      for (int mi : pmat)
+        if (std::find(order.begin(), order.end(), mi) == order.end()) order.push_back(mi);
+      for (int mi : order) {
+        RawMesh rm;
+        const auto& ml = mmat[id];
+        rm.material = (mi >= 0 && mi < (int)ml.size()) ? fbx_name(mats.at(ml[mi])->props[1].str) : "DefaultMaterial";
+        for (size_t k = 0; k < polys.size(); k++) {
+          if (pmat[k] != mi || polys[k].size() < 3) continue;
+          const int base = (int)rm.pos.size();
+          for (int v : polys[k]) rm.pos.push_back({(float)V[3 * v], (float)V[3 * v + 1], (float)V[3 * v + 2]});
+          const int n = (int)polys[k].size();
+          if (n == 3) {
+            rm.tris.push_back({base, base + 1, base + 2});
+          } else if (n == 4) {   // assimp Triangulate: start at a concave corner, if any
+            int sv = 0;
+            for (int i = 0; i < 4; i++) {
+              auto P3 = [&](int c) { return rm.pos[base + c]; };
+              const pm_float3 v = P3(i), v0 = P3((i + 3) % 4), v1 = P3((i + 2) % 4), v2 = P3((i + 1) % 4);
+              auto sub = [](pm_float3 a, pm_float3 c) { return pm_float3{a.x - c.x, a.y - c.y, a.z - c.z}; };
+              auto nrm = [](pm_float3 a) {
+                const float l = std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+                return l > 0.f ? pm_float3{a.x / l, a.y / l, a.z / l} : a;
+              };
+              auto dot = [](pm_float3 a, pm_float3 c) { return a.x * c.x + a.y * c.y + a.z * c.z; };
+              const pm_float3 left = nrm(sub(v0, v)), diag = nrm(sub(v1, v)), right = nrm(sub(v2, v));
+              const float ang = std::acos(dot(left, diag)) + std::acos(dot(right, diag));
+              if (ang > 3.14159265358979f) { sv = i; break; }
+            }
+            rm.tris.push_back({base + sv, base + (sv + 1) % 4, base + (sv + 2) % 4});
+            rm.tris.push_back({base + sv, base + (sv + 2) % 4, base + (sv + 3) % 4});
+          } else {
+            for (int k2 = 1; k2 + 1 < n; k2++) rm.tris.push_back({base, base + k2, base + k2 + 1});
+          }
+        }
+        nd.meshes.push_back((int)sc.meshes.size());
+        sc.meshes.push_back(std::move(rm));
+      }
+    }
+    const int me = (int)sc.nodes.size();
+    sc.nodes.push_back(nd);
+    node_of[id] = me;
+    for (int64_t k : mkids[id]) {
+      const int c = build_node(k);
+      if (c < 0) return -1;
+      sc.nodes[me].children.push_back(c);
+    }
+    return me;
+  };
+  RawNode root;
+  root.M = Mat4::identity();
+  sc.nodes.push_back(root);
+  sc.root = 0;
+  for (int64_t r : roots) {
+    const int c = build_node(r);
+    if (c < 0) return false;
+    sc.nodes[0].children.push_back(c);
+  }
+  return true;
+}
+
 std::string dir_of(const std::string& path) {
   const size_t s = path.find_last_of("/\\");
   return s == std::string::npos ? std::string(".") : path.substr(0, s);
@@ -468,7 +815,7 @@ extern "C" int pm_scene_data_load(const char* cpath, pm_scene_data** out) {
   std::string err;
   std::string ext = path.size() >= 4 ? path.substr(path.size() - 4) : "";
   for (char& c : ext) c = (char)std::tolower((unsigned char)c);
-  bool ok = ext == ".obj" ? load_obj(path, sc, err) : load_glb(path, sc, err);
+  bool ok = ext == ".obj" ? load_obj(path, sc, err) : ext == ".fbx" ? load_fbx(path, sc, err) : load_glb(path, sc, err);
   if (!ok) {
     std::fprintf(stderr, "pm: scene import failed: %s\n", err.c_str());
     return PM_ERR_IO;

@@ -130,10 +130,8 @@ __global__ void k_shard_bounds(const float4* __restrict__ elems, int64_t n, cons
   }
 }
 
-struct ShardSel {
-  int dim[16];
-  uint64_t prefix[16];   // key bits above `shift + 8` selected so far
-};
+// ShardSel (pm_internal.hpp): per segment the split dimension and the key bits
+// above `shift + 8` selected so far
 
 // segment -> (dim, prefix) in LDS (a by-value kernel argument indexed at run
 // time would go through private memory)
@@ -195,7 +193,7 @@ __global__ void k_shard_hist(const float4* __restrict__ elems, int64_t n, const 
 constexpr int kCompactIPT = 8;
 __global__ void k_shard_compact(const float4* __restrict__ elems, int64_t n, const float4* __restrict__ top, int l,
                                 ShardSel sel, int hb, const uint64_t* __restrict__ off,
-                                unsigned long long* __restrict__ cnt, uint64_t* __restrict__ cand) {
+                                unsigned long long* __restrict__ cnt, uint64_t* __restrict__ cand, uint64_t cap) {
   __shared__ ShardSelLds ss;
   __shared__ uint32_t lc[16];
   __shared__ unsigned long long lb[16];
@@ -229,7 +227,10 @@ __global__ void k_shard_compact(const float4* __restrict__ elems, int64_t n, con
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kCompactIPT; k++)
-      if (j[k] >= 0) cand[off[j[k]] + lb[j[k]] + mine[k]] = key[k];
+      if (j[k] >= 0) {
+        const uint64_t at = off[j[k]] + lb[j[k]] + mine[k];
+        if (at < cap) cand[at] = key[k];   // (a distributed selection fed wrong reductions)
+      }
   }
 }
 
@@ -390,7 +391,7 @@ hipError_t kd_shard_top(const float4* elems, int64_t n, int L, float4* top, std:
     if (!cand.p) return hipErrorOutOfMemory;
     PM_HIP_TRY(hipMemcpyAsync(off.p, ho.data(), 8 * nseg, hipMemcpyHostToDevice, s));
     PM_HIP_TRY(hipMemsetAsync(cnt.p, 0, 8 * nseg, s));
-    k_shard_compact<<<g, 256, 0, s>>>(elems, n, top, l, sel, 48, off.p, cnt.p, cand.p);
+    k_shard_compact<<<g, 256, 0, s>>>(elems, n, top, l, sel, 48, off.p, cnt.p, cand.p, (uint64_t)cand.n);
     PM_HIP_TRY(hipGetLastError());
     for (int pass = 2; pass < 8; pass++) {
       const int shift = 56 - 8 * pass;
@@ -416,6 +417,227 @@ hipError_t kd_shard_top(const float4* elems, int64_t n, int L, float4* top, std:
   }
   sizes = seg;
   return hipStreamSynchronize(s);
+}
+
+// ---- distributed top selection (each rank over its OWN photons) -------------
+// kd_shard_top reads every element on every rank: at 8 x 45.4 M photons that is
+// 16 full passes over 363 M elements per rank (34 ms), all of it replicated. The
+// same selection splits over the ranks: every pass (bounds, the two top-byte
+// histograms, the six candidate histograms) runs over the rank's own elements
+// -- its traced photons, with their GLOBAL indices, so keys and ties are those
+// of the gathered map -- and the caller reduces the small pass output across
+// ranks (MIN for the bounds, SUM for the histograms) before the next step. The
+// host logic is kd_shard_top's; the result (top nodes, subtree sizes) is the
+// same on every rank and equal to kd_shard_top's over the gathered elements.
+// It needs no exchanged photon, so it runs while the photon all-gather is in
+// flight. Top nodes carry only the split coordinate until the gathered
+// elements fill them in (kd_shard_top_fix).
+__device__ __forceinline__ float shard_kd_coord(float x) { return x != x ? __int_as_float(0x7f800000) : x; }
+
+__global__ void k_shard_local_elems(const pm_photon* __restrict__ a, int64_t na, int64_t aid,
+                                    const pm_photon* __restrict__ b, int64_t nb, int64_t bid,
+                                    float4* __restrict__ elems) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= na + nb) return;
+  const pm_photon p = i < na ? a[i] : b[i - na];
+  const int64_t id = i < na ? aid + i : bid + (i - na);
+  elems[i] = make_float4(shard_kd_coord(p.pos.x), shard_kd_coord(p.pos.y), shard_kd_coord(p.pos.z),
+                         __int_as_float((int)id));
+}
+
+// pass output -> the caller's int64 reduction buffer (bounds: maxima stored
+// inverted so that one MIN reduces both)
+__global__ void k_shard_red(const uint32_t* __restrict__ src, int count, int bounds, int64_t* __restrict__ red) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= count) return;
+  const uint32_t v = src[k];
+  red[k] = (int64_t)(bounds && (k % 6) >= 3 ? ~v : v);
+}
+
+__global__ void k_shard_top_fix(const float4* __restrict__ elems, int64_t ntop, float4* __restrict__ top) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntop) return;
+  const int w = __float_as_int(top[t].w);
+  const float4 e = elems[(uint32_t)w >> 2];
+  top[t] = make_float4(e.x, e.y, e.z, __int_as_float(w));
+}
+
+static float from_orderable(uint32_t u) {
+  const uint32_t bits = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+  float f;
+  std::memcpy(&f, &bits, 4);
+  return f;
+}
+
+hipError_t KdTopSel::init(const pm_photon* a, int64_t na, int64_t aid, const pm_photon* b, int64_t nb, int64_t bid,
+                          int64_t n_total, int levels, hipStream_t s) {
+  if (!shard_ok(n_total, levels)) return hipErrorInvalidValue;
+  L = levels;
+  n = na + nb;
+  seg_total = n_total;
+  seg.assign(1, n_total);
+  elems.alloc(std::max<int64_t>(n, 1));
+  top.alloc((size_t)1 << L);
+  ob.alloc(16 * 6);
+  hist.alloc(16 * 256);
+  off.alloc(16);
+  cnt.alloc(16);
+  if (!elems.p || !top.p || !ob.p || !hist.p || !off.p || !cnt.p) return hipErrorOutOfMemory;
+  if (n > 0) {
+    k_shard_local_elems<<<grid_for(n, 256), 256, 0, s>>>(a, na, aid, b, nb, bid, elems.p);
+    PM_HIP_TRY(hipGetLastError());
+  }
+  level = 0;
+  pending = -1;
+  return hipSuccess;
+}
+
+// issue pass `pending` of the current level into red (count, op)
+hipError_t KdTopSel::issue(int64_t* red, int64_t* count, int* op, hipStream_t s) {
+  const int nseg = 1 << level;
+  const int g = (int)std::max<int64_t>(1, std::min<int64_t>(kShardGrid, (n + 255) / 256));
+  if (pending == 0) {
+    std::vector<uint32_t> hb(nseg * 6);
+    for (int k = 0; k < nseg * 6; k++) hb[k] = (k % 6) < 3 ? 0xFFFFFFFFu : 0u;
+    PM_HIP_TRY(hipMemcpyAsync(ob.p, hb.data(), 4 * hb.size(), hipMemcpyHostToDevice, s));
+    if (n > 0) {
+      if (nseg <= 4) k_shard_bounds<4><<<g, 256, 0, s>>>(elems.p, n, top.p, level, ob.p);
+      else k_shard_bounds<0><<<g, 256, 0, s>>>(elems.p, n, top.p, level, ob.p);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    k_shard_red<<<grid_for(nseg * 6, 256), 256, 0, s>>>(ob.p, nseg * 6, 1, red);
+    *count = nseg * 6;
+    *op = 2;
+    return hipStreamSynchronize(s);   // hb is read by the copy
+  }
+  PM_HIP_TRY(hipMemsetAsync(hist.p, 0, 4 * 256 * nseg, s));
+  if (pending <= 2) {   // top-byte passes over the elements
+    if (n > 0) {
+      k_shard_hist<<<g, 256, 0, s>>>(elems.p, n, top.p, level, sel, 56 - 8 * (pending - 1), hist.p);
+      PM_HIP_TRY(hipGetLastError());
+    }
+  } else {   // candidate passes
+    const int shift = 56 - 8 * (pending - 1);
+    for (int j = 0; j < nseg; j++)
+      if (ncand[j] > 0)
+        k_shard_cand_hist<<<grid_for(ncand[j], 256), 256, 0, s>>>(cand.p + ho[j], ncand[j], sel.prefix[j], shift,
+                                                                   hist.p + 256 * j);
+    PM_HIP_TRY(hipGetLastError());
+  }
+  k_shard_red<<<grid_for(nseg * 256, 256), 256, 0, s>>>(hist.p, nseg * 256, 0, red);
+  PM_HIP_TRY(hipGetLastError());
+  *count = nseg * 256;
+  *op = 1;
+  return hipSuccess;
+}
+
+// consume the reduced output of pass `pending` (kd_shard_top's host logic)
+hipError_t KdTopSel::consume(const int64_t* red, hipStream_t s) {
+  const int nseg = 1 << level;
+  const int cnt_n = pending == 0 ? nseg * 6 : nseg * 256;
+  std::vector<int64_t> h(cnt_n);
+  PM_HIP_TRY(hipMemcpyAsync(h.data(), red, 8 * cnt_n, hipMemcpyDeviceToHost, s));
+  PM_HIP_TRY(hipStreamSynchronize(s));
+  if (pending == 0) {
+    rank.assign(nseg, 0);
+    for (int j = 0; j < nseg; j++) {
+      float ext[3];
+      for (int d = 0; d < 3; d++)
+        ext[d] = from_orderable((uint32_t)~(uint32_t)h[6 * j + 3 + d]) - from_orderable((uint32_t)h[6 * j + d]);
+      int dim = 0;
+      if (ext[1] > ext[dim]) dim = 1;
+      if (ext[2] > ext[dim]) dim = 2;
+      sel.dim[j] = dim;
+      sel.prefix[j] = 0;
+      rank[j] = left_size_host((int)seg[j]);
+    }
+    ncand.assign(nseg, 0);
+    pending = 1;
+    return hipSuccess;
+  }
+  const int shift = 56 - 8 * (pending - 1);
+  for (int j = 0; j < nseg; j++) {   // radix select: the bin holding rank j
+    int64_t r = rank[j];
+    int b = 0;
+    for (; b < 255; b++) {
+      if (r < h[256 * j + b]) break;
+      r -= h[256 * j + b];
+    }
+    rank[j] = r;
+    sel.prefix[j] |= (uint64_t)b << shift;
+    // top-byte passes: the global count under the prefix sizes the candidate
+    // buffer (candidate passes keep this rank's own count from the compaction)
+    if (pending <= 2) ncand[j] = h[256 * j + b];
+  }
+  if (pending == 2) {   // the local elements under each 16-bit prefix
+    std::vector<uint64_t> hc(nseg, 0);
+    PM_HIP_TRY(hipMemsetAsync(cnt.p, 0, 8 * nseg, s));
+    // local counts first: an upper bound (the global count) sizes the buffer
+    ho.assign(nseg, 0);
+    int64_t tot = 0;
+    for (int j = 0; j < nseg; j++) ho[j] = (uint64_t)tot, tot += ncand[j];
+    if ((int64_t)cand.n < std::max<int64_t>(tot, 1)) cand.alloc(std::max<int64_t>(tot, 1));
+    if (!cand.p) return hipErrorOutOfMemory;
+    PM_HIP_TRY(hipMemcpyAsync(off.p, ho.data(), 8 * nseg, hipMemcpyHostToDevice, s));
+    if (n > 0) {
+      const int g = (int)std::max<int64_t>(1, std::min<int64_t>(kShardGrid, (n + 255) / 256));
+      k_shard_compact<<<g, 256, 0, s>>>(elems.p, n, top.p, level, sel, 48, off.p, cnt.p, cand.p,
+                                          (uint64_t)cand.n);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    PM_HIP_TRY(hipMemcpyAsync(hc.data(), cnt.p, 8 * nseg, hipMemcpyDeviceToHost, s));
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    for (int j = 0; j < nseg; j++) ncand[j] = std::min<int64_t>((int64_t)hc[j], ncand[j]);   // this rank's own
+  }
+  if (pending < 8) {
+    pending++;
+    return hipSuccess;
+  }
+  // level done: the selected keys are the top nodes (split coordinate + tag);
+  // an index outside the map means the caller's reductions were not the
+  // documented ones (every rank, every pass): refuse it rather than place it
+  std::vector<float4> ht(nseg);
+  for (int j = 0; j < nseg; j++) {
+    const uint32_t id = (uint32_t)sel.prefix[j];
+    if ((int64_t)id >= seg_total) return hipErrorInvalidValue;
+    const float c = from_orderable((uint32_t)(sel.prefix[j] >> 32));
+    const uint32_t w = (id << 2) | (uint32_t)sel.dim[j];
+    float wf;
+    std::memcpy(&wf, &w, 4);
+    float4 r = make_float4(0.f, 0.f, 0.f, wf);
+    if (sel.dim[j] == 0) r.x = c;
+    else if (sel.dim[j] == 1) r.y = c;
+    else r.z = c;
+    ht[j] = r;
+  }
+  PM_HIP_TRY(hipMemcpyAsync(top.p + ((1 << level) - 1), ht.data(), sizeof(float4) * nseg, hipMemcpyHostToDevice, s));
+  PM_HIP_TRY(hipStreamSynchronize(s));
+  std::vector<int64_t> nxt;
+  for (int j = 0; j < nseg; j++) {
+    const int64_t ls = left_size_host((int)seg[j]);
+    nxt.push_back(ls);
+    nxt.push_back(seg[j] - ls - 1);
+  }
+  seg.swap(nxt);
+  level++;
+  pending = level < L ? 0 : -1;
+  return hipSuccess;
+}
+
+hipError_t KdTopSel::step(int64_t* red, int64_t* count, int* op, hipStream_t s) {
+  *count = 0;
+  *op = 0;
+  if (level >= L) return hipSuccess;
+  if (pending < 0) pending = 0;          // first call: level 0's bounds
+  else PM_HIP_TRY(consume(red, s));      // the caller reduced the previous pass
+  if (level >= L) return hipSuccess;     // finished
+  return issue(red, count, op, s);
+}
+
+hipError_t kd_shard_top_fix(const float4* elems, float4* top, int L, hipStream_t s) {
+  const int64_t ntop = (1ll << L) - 1;
+  k_shard_top_fix<<<grid_for(ntop, 64), 64, 0, s>>>(elems, ntop, top);
+  return hipGetLastError();
 }
 
 // Subtree j below the top L levels, in its local implicit layout with

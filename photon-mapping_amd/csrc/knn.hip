@@ -565,6 +565,12 @@ constexpr int kGatherQL = PM_GATHER_QL;   // LDS insert-queue depth
 #define PM_LEADER_BUDGET 2048
 #endif
 constexpr int kLeaderBudget = PM_LEADER_BUDGET;
+// 1: a leader cut off by the budget with a full list records its list's last
+// d^2 as its seed (followers and its own retry start from it); 0: no seed
+#ifndef PM_LEADER_SOFT
+#define PM_LEADER_SOFT 1
+#endif
+constexpr bool kLeaderSoft = PM_LEADER_SOFT;
 // Subtree-box skips in the k = 50 gather: 0 none, 1 leaders and retried
 // leaders, 2 every walk; boxes down to level D - PM_GATHER_BOX_SKIP (0: all).
 // Each walk switches to them after PM_BOX_AFTER wave iterations (knn_walk_lean).
@@ -699,8 +705,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
   const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   const v3 q = {qq.x, qq.y, qq.z};
   float cut = lean_cut(R2);
-  if (valid)
-    cut = (LEADERS || redo_lane) ? subtree_cut<WIDE>(nodes, (uint32_t)n, q, cut) : follower_cut(lead, nq, r, q, R2);
+  if (valid) {
+    if (LEADERS || redo_lane) {
+      cut = subtree_cut<WIDE>(nodes, (uint32_t)n, q, cut);
+      // a retried leader whose list was full when its budget ran out recorded
+      // that list's last d^2: its 50 points lie within it, so it bounds the
+      // 50th nearest (and admits it: only d^2 <= cut are candidates)
+      if (redo_lane && kLeaderSoft) {
+        const float t = lead[r / kSeedStride].w;
+        if (t >= 0.f) cut = fminf(cut, t);
+      }
+    } else {
+      cut = follower_cut(lead, nq, r, q, R2);
+    }
+  }
   double list[kKNearest];
   bool aborted;
   int knn_it = 0;
@@ -731,7 +749,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
   }
   if (LEADERS && kLeaderBudget > 0) {
     const bool redo = valid && aborted;
-    if (redo) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, -1.f);   // seeds nothing
+    // a cut-off walk's full list still bounds the 50th nearest (any 50 points
+    // do): its last d^2 seeds the followers and the retry; not full: nothing
+    const bool part_full = kLeaderSoft && gkey_word(list[kKNearest - 1]) != kNoWord;
+    if (redo) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, part_full ? gkey_d2(list[kKNearest - 1]) : -1.f);
     const uint64_t m = ballot(redo);
     if (m != 0) {   // wave-aggregated append to the retry list
       const int lane = threadIdx.x & 63, first = __ffsll((long long)m) - 1;

@@ -95,6 +95,32 @@ hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, int64_t n
                             int32_t* out, hipStream_t s);
 hipError_t kd_shard_assemble(const float4* elems, const float4* top, int L, const int32_t* tags,
                              const std::vector<int64_t>& sizes, float4* nodes, hipStream_t s);
+struct ShardSel {
+  int dim[16];
+  uint64_t prefix[16];   // key bits above `shift + 8` selected so far
+};
+// Distributed top selection (kdshard.hip): the rank's own photons with their
+// global indices (a: aid + i, b: bid + i); step() issues one pass into the
+// caller's int64 buffer (op 1: SUM, 2: MIN across ranks, 0: finished) after
+// consuming the caller's reduction of the previous one.
+struct KdTopSel {
+  DevBuf<float4> elems, top;
+  DevBuf<uint32_t> ob, hist;
+  DevBuf<uint64_t> off, cand;
+  DevBuf<unsigned long long> cnt;
+  int64_t n = 0;   // local elements
+  int64_t seg_total = 0;   // the gathered map's size
+  int L = 0, level = 0, pending = -1;   // pending: 0 bounds, 1-2 top-byte histograms, 3-8 candidate histograms
+  std::vector<int64_t> seg, rank, ncand;
+  std::vector<uint64_t> ho;
+  ShardSel sel{};
+  hipError_t init(const pm_photon* a, int64_t na, int64_t aid, const pm_photon* b, int64_t nb, int64_t bid,
+                  int64_t n_total, int levels, hipStream_t s);
+  hipError_t step(int64_t* red, int64_t* count, int* op, hipStream_t s);
+  hipError_t issue(int64_t* red, int64_t* count, int* op, hipStream_t s);
+  hipError_t consume(const int64_t* red, hipStream_t s);
+};
+hipError_t kd_shard_top_fix(const float4* elems, float4* top, int L, hipStream_t s);
 hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
                                      float pb, float4* elems, float4* payload, hipStream_t s);
 

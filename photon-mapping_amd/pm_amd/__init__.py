@@ -164,6 +164,12 @@ _SIGNATURES = {
     "pm_kd_shard_build": (C.c_int, [_P, C.c_int32, _P, _P]),
     "pm_photon_map_create_sharded": (C.c_int, [_P, _P, C.POINTER(_P), _P]),
     "pm_kd_shard_plan_destroy": (C.c_int, [_P]),
+    "pm_kd_top_sel_create": (C.c_int, [_P, C.c_int64, C.c_int64, _P, C.c_int64, C.c_int64, C.c_int64, C.c_int32,
+                                       C.POINTER(_P), _P]),
+    "pm_kd_top_sel_step": (C.c_int, [_P, _P, C.POINTER(C.c_int64), C.POINTER(C.c_int32), _P]),
+    "pm_kd_shard_plan_create_from_sel": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P, C.c_int64, C.c_float,
+                                                   C.POINTER(_P), _P]),
+    "pm_kd_top_sel_destroy": (C.c_int, [_P]),
     "pm_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_float, _P, _P, _P, _P]),
     "pm_gather": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P]),
     "pm_gather_k": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, _P, _P]),
@@ -502,13 +508,21 @@ class KdShardPlan:
     each rank builds its own (`build`), the caller all-gathers them and
     `map(all_subtrees)` places them (subtree order)."""
 
-    def __init__(self, a, power_a: float, b=None, power_b: float = 0.0, world: int = 1, stream=None):
+    def __init__(self, a, power_a: float, b=None, power_b: float = 0.0, world: int = 1, stream=None,
+                 sel: "KdTopSel" = None):
+        """sel: a finished KdTopSel (the distributed top selection) instead of
+        selecting the top levels here from the gathered photons."""
         h = _P()
         na = 0 if a is None else a.shape[0]
         nb = 0 if b is None else b.shape[0]
-        _check(_lib.pm_kd_shard_plan_create(_ptr(a) if na else None, na, float(power_a), _ptr(b) if nb else None,
-                                            nb, float(power_b), int(world), C.byref(h), _stream(stream)),
-               "pm_kd_shard_plan_create")
+        if sel is None:
+            _check(_lib.pm_kd_shard_plan_create(_ptr(a) if na else None, na, float(power_a),
+                                                _ptr(b) if nb else None, nb, float(power_b), int(world), C.byref(h),
+                                                _stream(stream)), "pm_kd_shard_plan_create")
+        else:
+            _check(_lib.pm_kd_shard_plan_create_from_sel(sel._h, _ptr(a) if na else None, na, float(power_a),
+                                                         _ptr(b) if nb else None, nb, float(power_b), C.byref(h),
+                                                         _stream(stream)), "pm_kd_shard_plan_create_from_sel")
         self._h = h
         self.n = na + nb
         cnt = C.c_int32(0)
@@ -539,6 +553,54 @@ class KdShardPlan:
     def close(self):
         if getattr(self, "_h", None):
             _lib.pm_kd_shard_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class KdTopSel:
+    """Distributed top selection (pm_kd_top_sel_*): this rank's own photons
+    (`a` / `b`, global indices a_first.. / b_first.. in the gathered map of
+    n_total photons) select the same top levels as KdShardPlan over the gathered
+    map, with `reduce(buf, op)` reducing each pass's small int64 output across
+    the ranks in place (op "sum" / "min"). Then KdShardPlan(..., sel=self)."""
+
+    def __init__(self, a, a_first: int, b, b_first: int, n_total: int, world: int, stream=None):
+        import torch
+        h = _P()
+        na = 0 if a is None else a.shape[0]
+        nb = 0 if b is None else b.shape[0]
+        _check(_lib.pm_kd_top_sel_create(_ptr(a) if na else None, na, int(a_first), _ptr(b) if nb else None, nb,
+                                         int(b_first), int(n_total), int(world), C.byref(h), _stream(stream)),
+               "pm_kd_top_sel_create")
+        self._h = h
+        self.buf = torch.empty((4096,), dtype=torch.int64, device="cuda")   # PM_KD_TOP_SEL_BUF
+        self.steps = 0
+
+    def step(self, stream=None):
+        """Consume the reduced previous pass, issue the next: (count, op) with op
+        None when finished, else "sum" / "min" over self.buf[:count]."""
+        cnt, op = C.c_int64(0), C.c_int32(0)
+        _check(_lib.pm_kd_top_sel_step(self._h, _ptr(self.buf), C.byref(cnt), C.byref(op), _stream(stream)),
+               "pm_kd_top_sel_step")
+        self.steps += 1
+        return cnt.value, {0: None, 1: "sum", 2: "min"}[op.value]
+
+    def run(self, reduce, stream=None):
+        """Drive every pass: reduce(view, op) reduces self.buf[:count] across ranks in place."""
+        while True:
+            cnt, op = self.step(stream)
+            if op is None:
+                return self
+            reduce(self.buf[:cnt], op)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.pm_kd_top_sel_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -51,6 +51,10 @@ class FrameConfig:
     # thread while the photons are traced and the maps built; it fills the
     # kd build's small, under-filled launches (config 3: ~0.6 ms per frame)
     overlap_render: bool = True
+    # N > 1: select the sharded build's top levels from each rank's own photons
+    # (pm_kd_top_sel, all-reduced passes) while the photon all-gather runs,
+    # instead of from all gathered photons on every rank
+    dist_top: bool = True
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -219,11 +223,72 @@ def shard_assemble(plan, everyone, world: int):
     return plan.map(torch.cat(parts))
 
 
-def sharded_map(pm, g, c, rank: int, world: int, dist):
-    """Global map (diffuse ++ caustic) built across ranks; returns (map, kd-build us
-    of this rank, the subtree all-gather included)."""
+def top_selection(pm, g_local, c_local, g_ns, c_ns, rank: int, world: int, dist, group=None):
+    """The global tree's top levels from this rank's OWN photons (pm_kd_top_sel):
+    every pass reads 1/G of the elements and its small output is all-reduced
+    (SUM / MIN), so it needs no exchanged photon and runs while the photon
+    all-gather is in flight (on `group`, a communicator of its own, so that
+    RCCL does not queue these small reductions behind the all-gather).
+    g_ns / c_ns: every rank's photon counts (the exchange's). Returns
+    (selection, us)."""
+    ops = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN}
+    g_first = sum(g_ns[:rank])
+    c_first = sum(g_ns) + sum(c_ns[:rank])
+    n_total = sum(g_ns) + sum(c_ns)
+    clock = _PhaseClock(g_local.device.type == "cuda")
+    sel = pm.KdTopSel(g_local, g_first, c_local, c_first, n_total, world)
+
+    def reduce(buf, op):
+        if group is not None:
+            dist.all_reduce(buf, op=ops[op], group=group)
+        else:
+            dist.all_reduce(buf, op=ops[op])
+    sel.run(reduce)
+    return sel, clock.stop_us()
+
+
+def simulated_top_selection(pm, g, c, world: int):
+    """top_selection of `world` ranks run in one process on one GPU (tests,
+    tools/kd_scale_probe.py): rank r holds shard_range(r) of g and of c, the
+    passes run rank after rank and the reductions are done here. Returns
+    (rank 0's selection, [us of each rank's passes])."""
     import torch
-    plan = pm.KdShardPlan(g, pm.PHOTON_POWER, c, pm.CAUSTICS_PHOTON_POWER, world=world)
+    ng, nc = g.shape[0], c.shape[0]
+    g_ns = [shard_range(ng, r, world)[1] - shard_range(ng, r, world)[0] for r in range(world)]
+    c_ns = [shard_range(nc, r, world)[1] - shard_range(nc, r, world)[0] for r in range(world)]
+    sels, us = [], [0.0] * world
+    for r in range(world):
+        g0, g1 = shard_range(ng, r, world)
+        c0, c1 = shard_range(nc, r, world)
+        t0 = time.perf_counter()
+        sels.append(pm.KdTopSel(g[g0:g1], g0, c[c0:c1], ng + c0, ng + nc, world))
+        torch.cuda.synchronize()
+        us[r] += (time.perf_counter() - t0) * 1e6
+    while True:
+        outs = []
+        for r, s in enumerate(sels):
+            t0 = time.perf_counter()
+            outs.append(s.step())
+            us[r] += (time.perf_counter() - t0) * 1e6
+        cnt, op = outs[0]
+        assert all(o == outs[0] for o in outs), outs   # every rank runs the same passes
+        if op is None:
+            break
+        stack = torch.stack([s.buf[:cnt] for s in sels])
+        red = stack.sum(0) if op == "sum" else stack.min(0).values
+        for s in sels:
+            s.buf[:cnt].copy_(red)
+    for s in sels[1:]:
+        s.close()
+    return sels[0], us
+
+
+def sharded_map(pm, g, c, rank: int, world: int, dist, sel=None):
+    """Global map (diffuse ++ caustic) built across ranks; returns (map, kd-build us
+    of this rank, the subtree all-gather included). sel: the finished
+    top_selection (else every rank selects the top levels from all photons)."""
+    import torch
+    plan = pm.KdShardPlan(g, pm.PHOTON_POWER, c, pm.CAUSTICS_PHOTON_POWER, world=world, sel=sel)
     us = pm.phase_us("kdbuild")
     if not plan.sizes:   # too small to split: every rank builds the whole tree
         m = plan.map()
@@ -274,10 +339,21 @@ class GpuBackend:
         self.phase["kdbuild"] = self.phase.get("kdbuild", 0.0) + pm.phase_us("kdbuild")
         return cm
 
-    def global_map(self, g, c, rank: int = 0, world: int = 1, dist=None):
+    def top_selection(self, g_local, c_local, g_ns, c_ns, rank: int, world: int, dist):
+        """The distributed top selection (None: not split across ranks)."""
+        if world < 2 or not self.cfg.shard_build or not self.cfg.dist_top:
+            return None
+        group = getattr(self, "_sel_group", None)
+        if group is None and hasattr(dist, "new_group") and not isinstance(dist, HostStagedDist):
+            group = self._sel_group = dist.new_group()
+        sel, us = top_selection(self.pm, g_local, c_local, g_ns, c_ns, rank, world, dist, group)
+        self.phase["kdbuild"] = self.phase.get("kdbuild", 0.0) + us
+        return sel
+
+    def global_map(self, g, c, rank: int = 0, world: int = 1, dist=None, sel=None):
         pm = self.pm
         if world > 1 and self.cfg.shard_build:
-            gm, kd = sharded_map(pm, g, c, rank, world, dist)
+            gm, kd = sharded_map(pm, g, c, rank, world, dist, sel=sel)
         else:
             gm = pm.PhotonMap(g, pm.PHOTON_POWER, c, pm.CAUSTICS_PHOTON_POWER)
             kd = pm.phase_us("kdbuild")
@@ -430,18 +506,24 @@ def _maps(backend, rank: int, world: int, dist, pending=None, early_caustic: boo
     c = backend.caustic_photons(pending) if pending is not None else backend.trace(True, rank, world)
     if backend.cfg.quantize:   # elementwise: the same before or after the exchange
         g, c = backend.quantize(g), backend.quantize(c)
+    sel = None
     if world > 1:
         # only position and colour reach the maps (kd nodes + gather payload):
         # 24 of the 40 bytes of a photon cross xGMI
         clock = _PhaseClock(g.device.type == "cuda")
-        c = unpack_rows(allgather_rows(pack_rows(c), world, dist))
-        xfer = allgather_rows_start(pack_rows(g), world, dist)
+        g_local, c_local = g, c
+        cx = allgather_rows_start(pack_rows(c_local), world, dist)
+        c = unpack_rows(cx.wait())
+        xfer = allgather_rows_start(pack_rows(g_local), world, dist)
         cm = backend.caustic_map(c)   # overlaps the global photons' transfer
+        if hasattr(backend, "top_selection"):   # so does the top selection (own photons only)
+            sel = backend.top_selection(g_local, c_local, xfer.ns, cx.ns, rank, world, dist)
         g = unpack_rows(xfer.wait())
         backend.phase["exchange"] = clock.stop_us()
     else:
         backend.phase["exchange"] = 0.0
         # None: start_render's thread builds it (frame() takes it before the render)
         cm = None if early_caustic else backend.caustic_map(c)
-    gm = backend.global_map(g, c, rank, world, dist)
+    gm = backend.global_map(g, c, rank, world, dist, sel=sel) if sel is not None else \
+        backend.global_map(g, c, rank, world, dist)
     return g, c, gm, cm

@@ -61,8 +61,8 @@ def test_status_strings():
     import pm_amd
     for s in range(9):
         assert pm_amd.lib.pm_status_string(s) != b"unknown status"
-    # 2: pm_render_params.caustic_k; 3: PM_ERR_DEVICE, pm_device_pool_stats
-    assert pm_amd.lib.pm_abi_version() == 3
+    # 2: pm_render_params.caustic_k; 3: PM_ERR_DEVICE, pm_device_pool_stats; 4: pm_kd_top_sel_*
+    assert pm_amd.lib.pm_abi_version() == 4
 
 
 def test_no_cpu_fallback_without_gpu(cornell):

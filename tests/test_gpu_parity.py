@@ -507,6 +507,50 @@ def test_sharded_kd_build_equals_replicated(cornell, world, data):
                        pm_amd.gather_photons(ref, q, brdf).view(torch.int32))
 
 
+@pytest.mark.parametrize("world", [2, 3, 8, 16])
+@pytest.mark.parametrize("data", ["cornell", "ties"])
+def test_distributed_top_selection_equals_replicated(cornell, world, data):
+    """the top levels selected from each rank's own photons
+    (pm_kd_top_sel: every pass over 1/G of the elements, its histograms
+    all-reduced; here the ranks run in one process and the reductions are done
+    on the host side of the test) give the same top nodes and subtree sizes as
+    the replicated selection over all photons, and the map built through them
+    equals the one-device map bit for bit (NaN positions included: +inf)."""
+    import pm_amd
+    from pm_amd import dist as pmdist
+    if data == "cornell":
+        meshes, lights = cornell
+        gs = pm_amd.Scene(meshes)
+        g = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, False)
+        c = pm_amd.run_point_light_ray_gen(gs, lights, 30000, 10, True)
+    else:
+        g, c = _synthetic_photons(70001, 5, grid=2.5), _synthetic_photons(999, 6, grid=2.5)
+        g[17, 1] = float("nan")   # sorts last in every pass, as in the one-device build
+    ref = pm_amd.PhotonMap(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER)
+    rep = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world)
+    sel, _ = pmdist.simulated_top_selection(pm_amd, g, c, world)
+    assert sel.steps > 1
+    plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world, sel=sel)
+    assert plan.sizes == rep.sizes and len(plan.sizes) > 0
+    bufs = [pmdist.shard_local(plan, r, world)[0] for r in range(world)]
+    m = pmdist.shard_assemble(plan, torch.cat(bufs), world)
+    assert torch.equal(m.export().view(torch.int32), ref.export().view(torch.int32))
+
+
+def test_distributed_top_selection_no_split(cornell):
+    """A map too small to split (or one rank) finishes at once: 0 subtrees, the
+    whole tree built in the map call, equal to the one-device build."""
+    import pm_amd
+    from pm_amd import dist as pmdist
+    g, c = _synthetic_photons(9, 1), _synthetic_photons(3, 2)
+    ref = pm_amd.PhotonMap(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER)
+    for world in (1, 8):
+        sel, _ = pmdist.simulated_top_selection(pm_amd, g, c, world)
+        plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world, sel=sel)
+        assert plan.sizes == []
+        assert torch.equal(plan.map().export().view(torch.int32), ref.export().view(torch.int32))
+
+
 def test_sharded_kd_build_small_map():
     """A map too small to split (n < 2^(L+1)) is built whole by every rank."""
     from pm_amd import dist as pmdist

@@ -289,3 +289,175 @@ def test_large_multigroup_obj(tmp_path):
         assert np.array_equal(m.vertices, v)
         assert np.array_equal(m.indices, ix)
         assert np.allclose(m.material, table.get(name, DEFAULT_MAT))
+
+
+# ---------------------------------------------------------------- FBX
+def test_fbx_cornell_matches_glb():
+    """assets/models/cornell-box/cornell-box.fbx (binary FBX 7400, the reference
+    reaches it through assimp, assetImporter.cxx:18-21) is the Cornell box of
+    cornell-box.glb exported at 100x: the same 9 meshes in the same order, the
+    same 58 triangles, each mesh's vertices within 1e-4 of the
+    GLB's after the 1/100 scale, the same triangles as position triples. The
+    FBX material names (floor, ..., "Right wall") are not the custom .mtl's
+    (floor.001, ...), so every mesh gets the white default, as the reference's
+    name lookup (assetImporter.cxx:191-204) would. Parity unpinned (assimp
+    cannot run here): the GLB is the check."""
+    f_meshes, f_lights = _load(os.path.join(S, "cornell-box", "cornell-box.fbx"))
+    g_meshes, g_lights = _load(os.path.join(S, "cornell-box", "cornell-box.glb"))
+    assert len(f_meshes) == len(g_meshes) == 9
+    assert sum(len(m.indices) for m in f_meshes) == 58
+    assert len(f_lights) == len(g_lights)
+    assert [m.name for m in f_meshes] == ["floor", "left_wall", "back_wall", "Right wall", "roof", "pink_cube",
+                                          "mirror", "glass", "white_cube"]
+    for fm, gm in zip(f_meshes, g_meshes):
+        assert gm.name.startswith(fm.name.lower().replace(" ", "_")), (fm.name, gm.name)
+        assert fm.vertices.shape == gm.vertices.shape and fm.indices.shape == gm.indices.shape
+        fv = fm.vertices.astype(np.float64) / 100.0
+        gv = gm.vertices.astype(np.float64)
+        d = np.sqrt(((fv[:, None, :] - gv[None, :, :]) ** 2).sum(-1))
+        assert d.min(0).max() < 1e-4 and d.min(1).max() < 1e-4, fm.name
+        tri = lambda v, idx: sorted(tuple(sorted(tuple(np.round(v[i], 2)) for i in t)) for t in idx)
+        assert tri(fv, fm.indices) == tri(gv, gm.indices), fm.name
+        assert np.allclose(fm.material, DEFAULT_MAT)
+
+
+def _fbx_node(name, props=(), kids=()):
+    """One FBX 7400 record (32-bit offsets) at offset 0; kids are pre-encoded
+    with relative offsets fixed up by _fbx_file."""
+    return (name, list(props), list(kids))
+
+
+def _fbx_encode(node, offset):
+    name, props, kids = node
+    pb = b""
+    for p in props:
+        if isinstance(p, bool):
+            pb += b"C" + struct.pack("<?", p)
+        elif isinstance(p, int):
+            pb += b"L" + struct.pack("<q", p)
+        elif isinstance(p, float):
+            pb += b"D" + struct.pack("<d", p)
+        elif isinstance(p, str):
+            s = p.encode().replace(b"::", b"\x00\x01")
+            pb += b"S" + struct.pack("<I", len(s)) + s
+        elif isinstance(p, tuple) and p[0] == "d":
+            raw = struct.pack("<%dd" % len(p[1]), *p[1])
+            pb += b"d" + struct.pack("<III", len(p[1]), 0, len(raw)) + raw
+        elif isinstance(p, tuple) and p[0] == "i":
+            raw = struct.pack("<%di" % len(p[1]), *p[1])
+            pb += b"i" + struct.pack("<III", len(p[1]), 0, len(raw)) + raw
+        else:
+            raise ValueError(p)
+    nm = name.encode()
+    head = 12 + 1 + len(nm)
+    body = b""
+    pos = offset + head + len(pb)
+    for k in kids:
+        kb = _fbx_encode(k, pos)
+        body += kb
+        pos += len(kb)
+    if kids:
+        body += b"\x00" * 13   # nested end marker
+    end = offset + head + len(pb) + len(body)
+    return struct.pack("<III", end, len(props), len(pb)) + bytes([len(nm)]) + nm + pb + body
+
+
+def _fbx_file(top):
+    out = b"Kaydara FBX Binary  \x00\x1a\x00" + struct.pack("<I", 7400)
+    for n in top:
+        out += _fbx_encode(n, len(out))
+    return out + b"\x00" * 13
+
+
+def _p70(**vals):
+    return _fbx_node("Properties70", [], [_fbx_node("P", [k, k, "", "A", *map(float, v)]) for k, v in vals.items()])
+
+
+def _model(mid, name, **trs):
+    return _fbx_node("Model", [mid, f"{name}::Model", "Mesh"], [_p70(**trs)])
+
+
+def _geometry(gid, name, verts, polys, mat=None):
+    idx = []
+    for p in polys:
+        idx += list(p[:-1]) + [~p[-1]]
+    kids = [_fbx_node("Vertices", [("d", [float(x) for x in np.ravel(verts)])]),
+            _fbx_node("PolygonVertexIndex", [("i", idx)])]
+    if mat is not None:
+        kids.append(_fbx_node("LayerElementMaterial", [0], [
+            _fbx_node("MappingInformationType", ["ByPolygon" if len(mat) > 1 else "AllSame"]),
+            _fbx_node("Materials", [("i", list(mat))])]))
+    return _fbx_node("Geometry", [gid, f"{name}::Geometry", "Mesh"], kids)
+
+
+def test_fbx_hierarchy_materials_and_quads(tmp_path):
+    """A synthetic binary FBX: a root model translated by (10, 0, 0) with a
+    child scaled by 2 (the reference composes node * parent,
+    assetImporter.cxx:43: the parent's transform applies first), a rotation
+    about z by 90 degrees (Euler XYZ, R = Rz Ry Rx), a two-material geometry
+    split into one mesh per material in first-appearance order, a concave quad
+    split at its reflex corner (assimp Triangulate) and a pentagon fan."""
+    sq = np.array([[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0]], np.float64)
+    dart = np.array([[0, 0, 0], [2, 1, 0], [0, 2, 0], [0.5, 1, 0]], np.float64)   # reflex corner at 3
+    pent = np.array([[0, 0, 0], [2, 0, 0], [3, 1, 0], [1, 2, 0], [-1, 1, 0]], np.float64)
+    two = np.concatenate([sq, sq + [0, 0, 1]])
+    objects = _fbx_node("Objects", [], [
+        _geometry(11, "g_sq", sq, [[0, 1, 2, 3]]),
+        _geometry(12, "g_two", two, [[0, 1, 2], [4, 5, 6], [0, 2, 3]], mat=[1, 0, 1]),
+        _geometry(13, "g_dart", dart, [[0, 1, 2, 3]]),
+        _geometry(14, "g_pent", pent, [[0, 1, 2, 3, 4]]),
+        _model(21, "root", **{"Lcl Translation": (10, 0, 0)}),
+        _model(22, "child", **{"Lcl Scaling": (2, 2, 2)}),
+        _model(23, "rot", **{"Lcl Rotation": (0, 0, 90)}),
+        _model(24, "shapes"),
+        _fbx_node("Material", [31, "red::Material", ""]),
+        _fbx_node("Material", [32, "blue::Material", ""]),
+    ])
+    C = lambda a, b: _fbx_node("C", ["OO", a, b])
+    conns = _fbx_node("Connections", [], [C(21, 0), C(23, 0), C(24, 0), C(22, 21), C(11, 21), C(12, 22),
+                                          C(31, 22), C(32, 22), C(11, 23), C(13, 24), C(14, 24)])
+    (tmp_path / "s.fbx").write_bytes(_fbx_file([_fbx_node("FBXHeaderExtension", [], [_fbx_node("FBXVersion", [7400])]),
+                                                objects, conns]))
+    (tmp_path / "lights.txt").write_text("0 20 0 1 1 1 10\n")
+    (tmp_path / "s.mtl").write_text("blue 0.1 0.2 0.9 1.0 0.0 0.0 1.0\n")
+    meshes, _ = _load(str(tmp_path / "s.fbx"))
+    # BFS: root's mesh, rot's mesh, shapes' two meshes, then child's two (material 1 = blue first)
+    assert [m.name for m in meshes] == ["DefaultMaterial", "DefaultMaterial", "DefaultMaterial", "DefaultMaterial",
+                                        "blue", "red"]
+    f32 = lambda a: np.asarray(a, np.float32)
+    assert np.array_equal(meshes[0].vertices, f32(sq + [10, 0, 0]))
+    assert meshes[0].indices.tolist() == [[0, 1, 2], [0, 2, 3]]
+    assert np.allclose(meshes[1].vertices, f32(np.stack([-sq[:, 1], sq[:, 0], sq[:, 2]], 1)), atol=1e-6)
+    # concave quad: start at the reflex corner 3 -> (3, 0, 1), (3, 1, 2)
+    dv = meshes[2].vertices
+    tris = [[tuple(dv[i]) for i in t] for t in meshes[2].indices]
+    assert tris == [[tuple(f32(dart[3])), tuple(f32(dart[0])), tuple(f32(dart[1]))],
+                    [tuple(f32(dart[3])), tuple(f32(dart[1])), tuple(f32(dart[2]))]]
+    assert len(meshes[3].indices) == 3   # pentagon fan
+    # child: node * parent -> scale first, then the parent's translation... applied as S(T(v))
+    blue_tris = 2 * (two[[0, 1, 2, 0, 2, 3]] + [10, 0, 0])
+    assert np.array_equal(np.sort(meshes[4].vertices, 0), np.sort(f32(np.unique(blue_tris, axis=0)), 0))
+    assert np.allclose(meshes[4].material, [0.1, 0.2, 0.9, 1.0, 0.0, 0.0, 1.0])
+    assert np.allclose(meshes[5].material, DEFAULT_MAT)
+    assert np.array_equal(np.sort(meshes[5].vertices, 0), np.sort(f32(2 * (two[4:7] + [10, 0, 0])), 0))
+
+
+@pytest.mark.parametrize("bad", ["magic", "truncated", "array_len", "pivot"])
+def test_malformed_fbx_rejected(tmp_path, bad):
+    import pm_amd
+    objects = _fbx_node("Objects", [], [_geometry(11, "g", TRI.astype(np.float64), [[0, 1, 2]]),
+                                        _model(21, "m", **({"RotationPivot": (1, 0, 0)} if bad == "pivot" else {}))])
+    conns = _fbx_node("Connections", [], [_fbx_node("C", ["OO", 21, 0]), _fbx_node("C", ["OO", 11, 21])])
+    blob = _fbx_file([objects, conns])
+    if bad == "magic":
+        blob = b"Kaydara FBX Ascii   " + blob[20:]
+    elif bad == "truncated":
+        blob = blob[: len(blob) // 2]
+    elif bad == "array_len":
+        i = blob.index(b"Vertices") + len(b"Vertices") + 1
+        blob = blob[:i] + struct.pack("<I", 1000) + blob[i + 4:]
+    (tmp_path / "x.fbx").write_bytes(blob)
+    (tmp_path / "lights.txt").write_text("0 20 0 1 1 1 10\n")
+    with pytest.raises(pm_amd.PMError) as e:
+        _load(str(tmp_path / "x.fbx"))
+    assert e.value.status == pm_amd.PM_ERR_IO

@@ -36,8 +36,23 @@ if os.environ.get("SHARD", "1") == "1":
         for rep in range(2):
             torch.cuda.synchronize()
             t0 = time.time()
-            plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world)
-            t_plan = pm_amd.phase_us("kdbuild") / 1e3
+            if os.environ.get("DIST", "1") == "1":
+                # distributed top selection: each rank's passes over its own shard
+                # (here rank after rank; the per-rank cost is the max), then the
+                # plan from the gathered photons (elements, top fix, classify)
+                sel, us = pmdist.simulated_top_selection(pm_amd, g, c, world)
+                torch.cuda.synchronize()
+                t1 = time.time()
+                plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world,
+                                          sel=sel)
+                torch.cuda.synchronize()
+                t_from = (time.time() - t1) * 1e3
+                t_plan = max(us) / 1e3 + t_from
+                print(f"  dist top selection: per-rank passes max {max(us) / 1e3:.1f} ms ({sel.steps} steps, "
+                      f"{sel.steps - 1} all-reduces), plan from gathered photons {t_from:.1f} ms", flush=True)
+            else:
+                plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world)
+                t_plan = pm_amd.phase_us("kdbuild") / 1e3
             bufs, t_sub = [], []
             for r in range(world):
                 b, us = pmdist.shard_local(plan, r, world)
