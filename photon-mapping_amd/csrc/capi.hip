@@ -741,21 +741,26 @@ int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* h, const pm_photon* a,
     }
     reset_phase(PH_KDBUILD);
     PhaseTimer tm(PH_KDBUILD, s);
-    e = launch_elems_from_photons(a, na, b, nb, pa, pb, p->elems.p, p->payload.p, s);
-    if (e == hipSuccess && h->split) {
+    if (!h->split) {
+      e = launch_elems_from_photons(a, na, b, nb, pa, pb, p->elems.p, p->payload.p, s);
+    } else {
+      // elements, payload and subtrees in one pass over the gathered photons
+      // (the selection's top nodes hold the split coordinates), then the top
+      // nodes' full positions from the elements
       const int L = h->sel.L;
       p->top.alloc((size_t)1 << L);
-      if (!p->top.p) e = hipErrorOutOfMemory;
+      p->sub.alloc(n);
+      if (!p->top.p || !p->sub.p) e = hipErrorOutOfMemory;
+      if (e == hipSuccess)
+        e = kd_shard_elems_classify(a, na, b, nb, pa, pb, h->sel.top.p, L, p->elems.p, p->payload.p, p->sub.p, s);
       if (e == hipSuccess)
         e = hipMemcpyAsync(p->top.p, h->sel.top.p, sizeof(float4) * (((size_t)1 << L) - 1), hipMemcpyDeviceToDevice,
                            s);
       if (e == hipSuccess) e = kd_shard_top_fix(p->elems.p, p->top.p, L, s);
       if (e == hipSuccess) {
         p->sizes = h->sel.seg;
-        p->sub.alloc(n);
-        e = p->sub.p ? kd_shard_classify(p->elems.p, n, L, p->top.p, p->sub.p, s) : hipErrorOutOfMemory;
+        p->L = L;
       }
-      if (e == hipSuccess) p->L = L;
     }
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -1033,6 +1033,9 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, B
 #ifndef PM_WIDE_STATS
 #define PM_WIDE_STATS 0
 #endif
+#ifndef PM_WIDE_DIAG
+#define PM_WIDE_DIAG 0   // timing diagnostics only (wrong results): 1 no final sorts, 2 no sorts at all
+#endif
 #if PM_WIDE_STATS
 // stats library only: [launch][0 groups, 1 iterations, 2 max iterations per group,
 // 3 flushes, 4 candidates, 5 valid lanes, 6 final keys]
@@ -1089,7 +1092,7 @@ __global__ __launch_bounds__(256) void k_gather_wide(const float4* __restrict__ 
           while (full) {
             const int l = __ffsll((long long)full) - 1;
             full &= full - 1;
-            const double tl = row_sort<S>(wrows + l * CAP, CAP, k, lane);
+            const double tl = PM_WIDE_DIAG == 2 ? tail : row_sort<S>(wrows + l * CAP, CAP, k, lane);
             if (lane == l) {
               cnt = k;
               tail = tl;
@@ -1117,9 +1120,7 @@ __global__ __launch_bounds__(256) void k_gather_wide(const float4* __restrict__ 
 #endif
     // final sort of every row: its first min(cnt, k) keys in (d^2, index) order
     fence_wave();
-#ifndef PM_WIDE_DIAG
-#define PM_WIDE_DIAG 0   // 1 (timing diagnostic only, wrong results): no final sorts
-#endif
+
     uint64_t live = PM_WIDE_DIAG ? 0 : ballot(cnt > 0);
     while (live) {
       const int l = __ffsll((long long)live) - 1;

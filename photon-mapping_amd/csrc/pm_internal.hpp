@@ -121,6 +121,9 @@ struct KdTopSel {
   hipError_t consume(const int64_t* red, hipStream_t s);
 };
 hipError_t kd_shard_top_fix(const float4* elems, float4* top, int L, hipStream_t s);
+hipError_t kd_shard_elems_classify(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
+                                   float pb, const float4* top, int L, float4* elems, float4* payload, uint8_t* sub,
+                                   hipStream_t s);
 hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
                                      float pb, float4* elems, float4* payload, hipStream_t s);
 

@@ -33,9 +33,30 @@ class OracleBackend:
     def caustic_map(self, c):
         return self.o.PhotonMap(c.numpy(), 0.5)
 
-    def global_map(self, g, c, rank=0, world=1, dist=None):
+    def top_selection(self, g_local, c_local, g_ns, c_ns, rank, world, dist):
+        """The distributed top selection's orchestration (pm_amd.dist.top_selection:
+        global offsets from the exchange's counts, SUM / MIN reductions of each
+        pass) with a protocol stand-in for pm_amd.KdTopSel."""
+        from pm_amd import dist as pmdist
+
+        class FakePm:
+            KdTopSel = _FakeTopSel
+        sel, _ = pmdist.top_selection(FakePm, g_local, c_local, g_ns, c_ns, rank, world, dist)
+        return sel
+
+    def global_map(self, g, c, rank=0, world=1, dist=None, sel=None):
         self.last = (g.numpy().copy(), c.numpy().copy())
+        if sel is not None:
+            # every rank's reductions cover the gathered map exactly once, and
+            # its global indices address its own rows in the gathered arrays
+            n = g.shape[0] + c.shape[0]
+            assert sel.total == [n, n * (n - 1) // 2, 0, -(n - 1)], (sel.total, n)
+            gc = torch.cat([g, c])[:, [0, 1, 2, 7, 8, 9]]   # what the exchange carries
+            for rows, first in ((sel.a, sel.a_first), (sel.b, sel.b_first)):
+                assert torch.equal(gc[first: first + rows.shape[0]], rows[:, [0, 1, 2, 7, 8, 9]])
+            self.sel_checked = True
         return self.o.PhotonMap(g.numpy(), 1.0, c.numpy(), 0.5)
+
 
     def render(self, gm, cm, tile_rank, tile_count, rgba):
         if rgba is not None:
@@ -44,6 +65,28 @@ class OracleBackend:
         img, _, _ = self.o.render(self.scene, self.cam, c.width, c.height, c.spp, c.depth, c.sky, self.lights, gm,
                                   cm, tile_rank=tile_rank, tile_count=tile_count, nthreads=2)
         return torch.from_numpy(img.view(np.int32).copy())
+
+
+class _FakeTopSel:
+    """Stand-in for pm_amd.KdTopSel with the same protocol (run(reduce) with
+    "sum" / "min" passes over self.buf): pass 1 sums (row count, sum of global
+    indices), pass 2 takes the min of (smallest index, -largest index)."""
+
+    def __init__(self, a, a_first, b, b_first, n_total, world):
+        self.a, self.a_first, self.b, self.b_first, self.n_total = a, a_first, b, b_first, n_total
+        self.buf = torch.zeros(4, dtype=torch.int64)
+
+    def run(self, reduce):
+        ids = list(range(self.a_first, self.a_first + self.a.shape[0])) + \
+            list(range(self.b_first, self.b_first + self.b.shape[0]))
+        self.buf[0], self.buf[1] = len(ids), sum(ids)
+        reduce(self.buf[:2], "sum")
+        first = self.buf[:2].tolist()
+        self.buf[0] = min(ids) if ids else self.n_total
+        self.buf[1] = -max(ids) if ids else 0
+        reduce(self.buf[:2], "min")
+        self.total = first + self.buf[:2].tolist()
+        return self
 
 
 def _cfg():
@@ -65,6 +108,7 @@ def _worker(rank, world, port, q):
         # zero it before the tile render, or the SUM-reduce would add stale pixels
         stale = torch.full((cfg.height, cfg.width), 7, dtype=torch.int32)
         rgba, info = pmdist.frame(be, rank, world, dist, stale)
+        assert getattr(be, "sel_checked", False)   # the distributed top selection ran (N > 1)
         g, c = be.last
         q.put((rank, rgba.numpy().copy() if rank == 0 else None, g, c, info["n_global"]))
     finally:
