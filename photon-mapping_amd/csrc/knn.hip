@@ -589,6 +589,11 @@ constexpr bool kLeaderSoft = PM_LEADER_SOFT;
 #define PM_GATHER_BOX_SKIP 0
 #endif
 constexpr int kGatherBox = PM_GATHER_BOX;
+// 1 (test variant): 64-bit node addressing for every map, so the path that
+// maps of >= 2^28 nodes take runs on the small parity workloads
+#ifndef PM_FORCE_WIDE
+#define PM_FORCE_WIDE 0
+#endif
 #ifndef PM_BOX_AFTER
 #define PM_BOX_AFTER 512
 #endif
@@ -860,7 +865,7 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   const int rb = kLeaderBudget > 0 ? grid_for(nl, 256) : 0;   // retry workgroups: one lane per leader
   const int gl = grid_for(nl, 256), gf = grid_for(nq - nl, 256) + rb;
   // node byte offsets fit 32 bits below 2^28 nodes (saddr loads); larger maps use 64-bit addresses
-  const bool wide = n >= (1 << 28);
+  const bool wide = PM_FORCE_WIDE || n >= (1 << 28);
 #define PM_LEVELS(T, W)                                                                                          \
   k_gather_level<T, true, W><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, retry.p, \
                                                 nretry.p, 0, bx);                                               \
@@ -1191,7 +1196,7 @@ static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb,
     PM_HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wide_stats), zero, sizeof(zero), 0, hipMemcpyHostToDevice, s));
   }
 #endif
-  const bool wide = n >= (1 << 28);
+  const bool wide = PM_FORCE_WIDE || n >= (1 << 28);
 #define PM_WIDE_LAUNCH(W)                                                                                          \
   k_gather_wide<0, true, W, S><<<(int)std::min<int64_t>(wg, (nl + 255) / 256), 256, 0, s>>>(                     \
       m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p, nl, bx);                              \

@@ -91,6 +91,9 @@ def run(full: bool = False) -> dict:
     em, _ = pm_amd.load_photons(empty, empty)
     for name, m in (("g", gm), ("c", cm), ("e", em)):
         out[f"gather_{name}"] = pm_amd.gather_photons(m, qt, bt).cpu().numpy()
+    # the collect-and-sort gather (k > 64): 8- and 16-key rows
+    for k in (200, 256):
+        out[f"gather_k{k}"] = pm_amd.gather_photons(gm, qt, bt, k=k).cpu().numpy()
     out["knn_ids"], out["knn_d2"], out["knn_md"] = [x.cpu().numpy() for x in pm_amd.knn(gm, qt[:5000], k=50)]
     for W, H, spp in ((64, 48, 2), (40, 30, 1)):
         cam = pm_amd.setup_camera(*CAM, W, H)
