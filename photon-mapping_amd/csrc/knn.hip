@@ -572,7 +572,9 @@ constexpr int kLeaderBudget = PM_LEADER_BUDGET;
 #endif
 constexpr bool kLeaderSoft = PM_LEADER_SOFT;
 // Subtree-box skips in the k = 50 gather: 0 none, 1 leaders and retried
-// leaders, 2 every walk; boxes down to level D - PM_GATHER_BOX_SKIP (0: all).
+// leaders, 2 every walk, 3 every walk but the budgeted leaders' (whose long
+// walks the retry workgroups redo with boxes; the leader launch keeps 4
+// waves/SIMD); boxes down to level D - PM_GATHER_BOX_SKIP (0: all).
 // Each walk switches to them after PM_BOX_AFTER wave iterations (knn_walk_lean).
 // Measured (round 3, ms per frame, config 2 / config 3): none 21.4 / 108.7;
 // every walk from the start 9.8 / 122.9 (config 3's global gather 41.6 ->
@@ -582,8 +584,11 @@ constexpr bool kLeaderSoft = PM_LEADER_SOFT;
 // 111.7 / 108.8 / 108.5: 512 (config 2's global gather 16.3 -> 4.3 ms: the
 // long Cornell walks along the box walls end, config 3's walks mostly finish
 // before the switch).
+// Round 3, every walk after 512 vs every walk but the leaders' (mode 3, kept):
+// config 3 109.2 / 108.9 vs 107.8 / 108.4 ms (the leader launch keeps 4
+// waves/SIMD instead of 3), config 2 9.01 vs 9.07 ms.
 #ifndef PM_GATHER_BOX
-#define PM_GATHER_BOX 2
+#define PM_GATHER_BOX 3
 #endif
 #ifndef PM_GATHER_BOX_SKIP
 #define PM_GATHER_BOX_SKIP 0
@@ -683,7 +688,7 @@ __device__ __forceinline__ float subtree_cut(const float4* __restrict__ nodes, u
 // kernel symbol (rocprof). perm: lane of walk rank r takes query perm[r] and
 // writes its result there (Morton walk order without permuted copies).
 template <int TAG, bool LEADERS, bool WIDE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && kGatherBox ? 3 : 4))) void k_gather_level(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && (kGatherBox == 1 || kGatherBox == 2) ? 3 : 4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
     uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx) {
@@ -728,7 +733,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
   bool aborted;
   int knn_it = 0;
   int* const itp = PM_KNN_STATS ? &knn_it : nullptr;
-  if (kGatherBox == 2 || (kGatherBox == 1 && LEADERS)) {
+  if (kGatherBox == 2 || (kGatherBox == 1 && LEADERS) || (kGatherBox == 3 && !LEADERS)) {
     aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0, kBoxAfter>(
         nodes, n, q, cut, valid, list, lq + threadIdx.x, 256, bx, itp);
   } else if (kGatherBox == 1 && redo_lane) {   // block-uniform: the retried leaders
@@ -1047,8 +1052,13 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, B
 __device__ unsigned long long g_wide_stats[2][8];
 #endif
 
+// occupancy target of the wide kernels (0: the compiler's choice, 4 waves/SIMD
+// at ~101 VGPRs; A/B knob)
+#ifndef PM_WIDE_WAVES
+#define PM_WIDE_WAVES 0
+#endif
 template <int TAG, bool LEADERS, bool WIDE, int S>
-__global__ __launch_bounds__(256) void k_gather_wide(const float4* __restrict__ nodes,
+__global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wide(const float4* __restrict__ nodes,
                                                      const float4* __restrict__ payload, int n,
                                                      const float4* __restrict__ qb, int64_t nq,
                                                      float4* __restrict__ out, const uint32_t* __restrict__ perm,
