@@ -859,13 +859,62 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   if (kLeaderBudget > 0) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, sizeof(uint32_t), s));
   DevBuf<float4> box(kGatherBox ? 2 * (size_t)std::max<int64_t>(boxed_nodes(n, PM_GATHER_BOX_SKIP), 1) : 0);
   BoxView bx;
+  hipEvent_t box_done = nullptr;
   if (kGatherBox) {
     if (!box.p) return hipErrorOutOfMemory;
     int64_t nbox = 0;
-    PM_HIP_TRY(build_subtree_boxes(m->nodes.p, n, PM_GATHER_BOX_SKIP, box.p, &nbox, s));
+    // mode 3: the leader launch reads no box, so the boxes are built beside it
+    // on a side stream (config 3: 43 small launches, ~0.9 ms); the follower
+    // launch waits for them. The buffer goes back to s's pool when this call
+    // returns; s's next use of it comes after the follower launch, which
+    // waits for the build.
+    hipStream_t bs = kGatherBox == 3 ? side_stream(stream_device(s), 1) : nullptr;
+    hipEvent_t nodes_ready = nullptr;
+    if (bs && (hipEventCreateWithFlags(&nodes_ready, hipEventDisableTiming) != hipSuccess ||
+               hipEventCreateWithFlags(&box_done, hipEventDisableTiming) != hipSuccess)) {
+      (void)hipGetLastError();
+      if (nodes_ready) (void)hipEventDestroy(nodes_ready);
+      nodes_ready = box_done = nullptr;
+      bs = nullptr;
+    }
+    hipError_t e = hipSuccess;
+    if (bs) {
+      e = hipEventRecord(nodes_ready, s);
+      if (e == hipSuccess) e = hipStreamWaitEvent(bs, nodes_ready, 0);
+      if (e == hipSuccess) e = build_subtree_boxes(m->nodes.p, n, PM_GATHER_BOX_SKIP, box.p, &nbox, bs);
+      if (e == hipSuccess) e = hipEventRecord(box_done, bs);
+      (void)hipEventDestroy(nodes_ready);
+      if (e != hipSuccess) {
+        (void)hipStreamSynchronize(bs);   // nothing on the side stream outlives a failed call
+        (void)hipEventDestroy(box_done);
+        return e;
+      }
+    } else {
+      PM_HIP_TRY(build_subtree_boxes(m->nodes.p, n, PM_GATHER_BOX_SKIP, box.p, &nbox, s));
+    }
     bx.box = box.p;
     bx.nbox = (uint32_t)nbox;
   }
+  // an early return still leaves s waiting for the build before the buffer
+  // goes back to s's pool (the guard is destroyed before `box`)
+  struct BoxWait {
+    hipStream_t s;
+    hipEvent_t& e;
+    ~BoxWait() {
+      if (e) {
+        (void)hipStreamWaitEvent(s, e, 0);
+        (void)hipEventDestroy(e);
+      }
+    }
+  } box_wait{s, box_done};
+  // the follower launch (and anything after it on s) waits for the boxes
+  auto boxes_ready = [&]() -> hipError_t {
+    if (!box_done) return hipSuccess;
+    const hipError_t e = hipStreamWaitEvent(s, box_done, 0);
+    (void)hipEventDestroy(box_done);
+    box_done = nullptr;
+    return e;
+  };
   // followers (+ the retry workgroups first, with a leader budget)
   const int rb = kLeaderBudget > 0 ? grid_for(nl, 256) : 0;   // retry workgroups: one lane per leader
   const int gl = grid_for(nl, 256), gf = grid_for(nq - nl, 256) + rb;
@@ -875,6 +924,7 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   k_gather_level<T, true, W><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, retry.p, \
                                                 nretry.p, 0, bx);                                               \
   PM_HIP_TRY(hipGetLastError());                                                                                \
+  PM_HIP_TRY(boxes_ready());                                                                                    \
   if (nq > nl || kLeaderBudget > 0)                                                                             \
   k_gather_level<T, false, W><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, retry.p, \
                                                  nretry.p, rb, bx)

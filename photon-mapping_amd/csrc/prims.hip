@@ -136,18 +136,19 @@ void dev_pool_stats(int dev, size_t* live, size_t* cached) {
 // One non-blocking side stream per device for the life of the process (the
 // render's caustic gather): its allocator pool then persists from frame to
 // frame (a per-job stream took its temporaries' pool with it).
-hipStream_t side_stream(int dev) {
+hipStream_t side_stream(int dev, int idx) {
   static std::mutex mu;
-  static std::map<int, hipStream_t> streams;
+  static std::map<std::pair<int, int>, hipStream_t> streams;
   std::lock_guard<std::mutex> lk(mu);
-  auto it = streams.find(dev);
+  const std::pair<int, int> key{dev, idx};
+  auto it = streams.find(key);
   if (it != streams.end()) return it->second;
   hipStream_t s = nullptr;
   if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
-  streams[dev] = s;
+  streams[key] = s;
   return s;
 }
 

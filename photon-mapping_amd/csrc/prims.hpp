@@ -32,8 +32,9 @@ struct AllocStream {
 void dev_free(void* p);
 // Bytes held by live blocks and by idle pooled blocks of device `dev` (-1: all).
 void dev_pool_stats(int dev, size_t* live, size_t* cached);
-// The process-wide side stream of a device (created on first use).
-hipStream_t side_stream(int dev);
+// The process-wide side stream `idx` of a device (created on first use): 0
+// the render's caustic gather, 1 the global gather's box build.
+hipStream_t side_stream(int dev, int idx = 0);
 void dev_cache_trim();
 
 template <typename T>
