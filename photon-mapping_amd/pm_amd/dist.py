@@ -55,6 +55,10 @@ class FrameConfig:
     # (pm_kd_top_sel, all-reduced passes) while the photon all-gather runs,
     # instead of from all gathered photons on every rank
     dist_top: bool = True
+    # one rank: run the caustic gather on the render side thread right after
+    # the caustic map (pm_render_gather_caustic), i.e. beside the global map's
+    # kd build, instead of beside the global gather in finish
+    early_caustic_gather: bool = False
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -402,6 +406,8 @@ class GpuBackend:
                     if caustic_map:
                         cm = pm.PhotonMap(t, pm.CAUSTICS_PHOTON_POWER, stream=side.cuda_stream)
                         box["cm"] = (cm, pm.phase_us("kdbuild"))
+                        if c.early_caustic_gather:
+                            job.gather_caustic(cm, stream=side.cuda_stream)
             except BaseException as e:   # re-raised by finish_render / join_render
                 box["e"] = e
             finally:
