@@ -1053,10 +1053,17 @@ __device__ __forceinline__ double row_sort(double* __restrict__ row, int cnt, in
 // One collect step of every lane: lean_step's walk and point test (with the
 // subtree-box skip), the candidate appended to the lane's row instead of an
 // LDS insert queue.
+// PM_WIDE_STAGE: candidates are staged 8 at a time in an LDS column of the
+// lane (`stage`, slot j at stage[j * 256]) and reach the row as one 64-B chunk
+// (4 x 16-B stores) when the 8th arrives: one 8-B store per candidate left
+// rows partly filled in L2 (22 GB written for 7.7 GB of keys, config 5).
+#ifndef PM_WIDE_STAGE
+#define PM_WIDE_STAGE 1
+#endif
 template <bool WIDE>
 __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, BoxView bx, uint32_t n, v3 q,
                                              double tail, LeanWalk& w, float4& nd, float4& ba, float4& bb,
-                                             double* __restrict__ row, int& cnt) {
+                                             double* __restrict__ row, int& cnt, double* stage = nullptr) {
   const uint32_t word = __float_as_uint(nd.w);
   const uint32_t dim = word & 3u;
   const float dx = q.x - nd.x, dy = q.y - nd.y, dz = q.z - nd.z;
@@ -1082,7 +1089,18 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, B
   const bool cand = w.walking && test && key < tail;
   w.far_mask = stay ? (w.far_mask << 1 | (farok ? 1u : 0u)) : w.far_mask >> w.j1;
   w.up = !stay;
-  if (cand) row[cnt] = key;
+  if (PM_WIDE_STAGE) {
+    if (cand) {
+      stage[(cnt & 7) * 256] = key;
+      if ((cnt & 7) == 7) {   // the 8th: the chunk [cnt - 7, cnt] goes out in one piece
+        double2* dst = reinterpret_cast<double2*>(row + (cnt & ~7));
+#pragma unroll
+        for (int j = 0; j < 4; j++) dst[j] = make_double2(stage[(2 * j) * 256], stage[(2 * j + 1) * 256]);
+      }
+    }
+  } else if (cand) {
+    row[cnt] = key;
+  }
   cnt += cand ? 1 : 0;
   w.c1 = c1n;
   w.walking = go;
@@ -1094,7 +1112,8 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, B
 #define PM_WIDE_STATS 0
 #endif
 #ifndef PM_WIDE_DIAG
-#define PM_WIDE_DIAG 0   // timing diagnostics only (wrong results): 1 no final sorts, 2 no sorts at all
+#define PM_WIDE_DIAG 0   // timing diagnostics only (wrong results): 1 no final sorts, 2 no sorts at all,
+                         // 3 no sorts, an overflowing row stops its lane
 #endif
 #if PM_WIDE_STATS
 // stats library only: [launch][0 groups, 1 iterations, 2 max iterations per group,
@@ -1115,10 +1134,18 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
                                                      float4* __restrict__ lead, int k, double* __restrict__ rows,
                                                      uint32_t* __restrict__ counter, int64_t nitems, BoxView bx) {
   constexpr int CAP = 64 * S;
+  static_assert(CAP % 8 == 0, "rows hold whole 8-key chunks");
   const float R2 = kKMaxDistance * kKMaxDistance;
   const int lane = threadIdx.x & 63;
   double* const wrows = rows + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * CAP;
   double* const row = wrows + lane * CAP;
+  __shared__ double stage_lds[PM_WIDE_STAGE ? 8 * 256 : 1];
+  double* const stage = stage_lds + threadIdx.x;
+  // this lane's staged keys (cnt & 7 of them) into its row
+  auto spill_stage = [&](int cnt) {
+    if (PM_WIDE_STAGE)
+      for (int j = 0; j < (cnt & 7); j++) row[(cnt & ~7) + j] = stage[j * 256];
+  };
   for (;;) {
     uint32_t g = 0;
     if (lane == 0) g = atomicAdd(counter, 1u);
@@ -1145,8 +1172,9 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
 #if PM_WIDE_STATS
         const int c0 = cnt;
 #endif
-        collect_step<WIDE>(nodes, bx, (uint32_t)n, q, tail, w, nd, ba, bb, row, cnt);
+        collect_step<WIDE>(nodes, bx, (uint32_t)n, q, tail, w, nd, ba, bb, row, cnt, stage);
         uint64_t full = ballot(cnt == CAP);
+        const uint64_t full0 = full;
 #if PM_WIDE_STATS
         it++;
         fl += __popcll(full);
@@ -1157,14 +1185,20 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
           while (full) {
             const int l = __ffsll((long long)full) - 1;
             full &= full - 1;
-            const double tl = PM_WIDE_DIAG == 2 ? tail : row_sort<S>(wrows + l * CAP, CAP, k, lane);
+            const double tl = PM_WIDE_DIAG >= 2 ? tail : row_sort<S>(wrows + l * CAP, CAP, k, lane);
             if (lane == l) {
               cnt = k;
               tail = tl;
               w.bound = gkey_d2(tl);
+              if (PM_WIDE_DIAG == 3) w.walking = false;   // diagnostic: an overflowing lane stops
             }
           }
           fence_wave();
+          // a full row was flushed chunk by chunk (CAP % 8 == 0); the kept k
+          // keys end mid-chunk unless 8 | k: that chunk's head goes back to the
+          // stage, so the next chunk write carries it
+          if (PM_WIDE_STAGE && (k & 7) && full0 & (1ull << lane))
+            for (int j = 0; j < (k & 7); j++) stage[j * 256] = row[(k & ~7) + j];
         }
         if (ballot(w.walking) == 0) break;
       }
@@ -1184,6 +1218,7 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
     atomicAdd(&g_wide_stats[LEADERS][6], (unsigned long long)cnt);
 #endif
     // final sort of every row: its first min(cnt, k) keys in (d^2, index) order
+    spill_stage(cnt);
     fence_wave();
 
     uint64_t live = PM_WIDE_DIAG ? 0 : ballot(cnt > 0);
