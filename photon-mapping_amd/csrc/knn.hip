@@ -1053,13 +1053,19 @@ __device__ __forceinline__ double row_sort(double* __restrict__ row, int cnt, in
 // One collect step of every lane: lean_step's walk and point test (with the
 // subtree-box skip), the candidate appended to the lane's row instead of an
 // LDS insert queue.
-// PM_WIDE_STAGE: candidates are staged 8 at a time in an LDS column of the
-// lane (`stage`, slot j at stage[j * 256]) and reach the row as one 64-B chunk
-// (4 x 16-B stores) when the 8th arrives: one 8-B store per candidate left
-// rows partly filled in L2 (22 GB written for 7.7 GB of keys, config 5).
+// PM_WIDE_STAGE: candidates are staged PM_WIDE_CHUNK at a time in an LDS
+// column of the lane (`stage`, slot j at stage[j * 256]) and reach the row as
+// one chunk (16-B stores) when its last key arrives: one 8-B store per
+// candidate left rows partly filled in L2 (22 GB written for 7.7 GB of keys,
+// config 5; staging 8: caustic gather 25.1 -> 20.6 ms).
 #ifndef PM_WIDE_STAGE
 #define PM_WIDE_STAGE 1
 #endif
+#ifndef PM_WIDE_CHUNK
+#define PM_WIDE_CHUNK 8   // keys per staged chunk (8: 64 B, 16: one 128-B line)
+#endif
+constexpr int kChunkKeys = PM_WIDE_CHUNK;
+static_assert(kChunkKeys == 8 || kChunkKeys == 16, "chunk of 8 or 16 keys");
 template <bool WIDE>
 __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, BoxView bx, uint32_t n, v3 q,
                                              double tail, LeanWalk& w, float4& nd, float4& ba, float4& bb,
@@ -1090,12 +1096,14 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, B
   w.far_mask = stay ? (w.far_mask << 1 | (farok ? 1u : 0u)) : w.far_mask >> w.j1;
   w.up = !stay;
   if (PM_WIDE_STAGE) {
+    constexpr int M = kChunkKeys - 1;
     if (cand) {
-      stage[(cnt & 7) * 256] = key;
-      if ((cnt & 7) == 7) {   // the 8th: the chunk [cnt - 7, cnt] goes out in one piece
-        double2* dst = reinterpret_cast<double2*>(row + (cnt & ~7));
+      stage[(cnt & M) * 256] = key;
+      if ((cnt & M) == M) {   // the last of a chunk: [cnt - M, cnt] goes out in one piece
+        double2* dst = reinterpret_cast<double2*>(row + (cnt & ~M));
 #pragma unroll
-        for (int j = 0; j < 4; j++) dst[j] = make_double2(stage[(2 * j) * 256], stage[(2 * j + 1) * 256]);
+        for (int j = 0; j < kChunkKeys / 2; j++)
+          dst[j] = make_double2(stage[(2 * j) * 256], stage[(2 * j + 1) * 256]);
       }
     }
   } else if (cand) {
@@ -1121,6 +1129,15 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, B
 __device__ unsigned long long g_wide_stats[2][8];
 #endif
 
+// Leader step budget of the wide gather (wave iterations; 0: none): the
+// leader launch is a few thousand waves on an otherwise idle GPU, so its length
+// is its slowest wave's (config 5: 1,665 iterations per leader wave on
+// average, 4,557 at most); lanes still walking at the budget are redone at the
+// head of the follower launch, beside the followers.
+#ifndef PM_WIDE_LEADER_BUDGET
+#define PM_WIDE_LEADER_BUDGET 2048
+#endif
+constexpr int kWideLeaderBudget = PM_WIDE_LEADER_BUDGET;
 // occupancy target of the wide kernels (0: the compiler's choice, 4 waves/SIMD
 // at ~101 VGPRs; A/B knob)
 #ifndef PM_WIDE_WAVES
@@ -1132,36 +1149,55 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
                                                      const float4* __restrict__ qb, int64_t nq,
                                                      float4* __restrict__ out, const uint32_t* __restrict__ perm,
                                                      float4* __restrict__ lead, int k, double* __restrict__ rows,
-                                                     uint32_t* __restrict__ counter, int64_t nitems, BoxView bx) {
+                                                     uint32_t* __restrict__ counter, int64_t nitems, BoxView bx,
+                                                     uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry) {
   constexpr int CAP = 64 * S;
-  static_assert(CAP % 8 == 0, "rows hold whole 8-key chunks");
+  static_assert(CAP % kChunkKeys == 0, "rows hold whole chunks");
   const float R2 = kKMaxDistance * kKMaxDistance;
   const int lane = threadIdx.x & 63;
   double* const wrows = rows + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * CAP;
   double* const row = wrows + lane * CAP;
-  __shared__ double stage_lds[PM_WIDE_STAGE ? 8 * 256 : 1];
+  __shared__ double stage_lds[PM_WIDE_STAGE ? kChunkKeys * 256 : 1];
   double* const stage = stage_lds + threadIdx.x;
   // this lane's staged keys (cnt & 7 of them) into its row
   auto spill_stage = [&](int cnt) {
+    constexpr int M = kChunkKeys - 1;
     if (PM_WIDE_STAGE)
-      for (int j = 0; j < (cnt & 7); j++) row[(cnt & ~7) + j] = stage[j * 256];
+      for (int j = 0; j < (cnt & M); j++) row[(cnt & ~M) + j] = stage[j * 256];
   };
+  // follower launch: the leaders that ran out of budget come first (their
+  // count is the leader launch's, complete before this launch starts)
+  const int64_t nre = (!LEADERS && kWideLeaderBudget > 0) ? (int64_t)*nretry : 0;
+  const int64_t items = nitems + nre;
   for (;;) {
     uint32_t g = 0;
     if (lane == 0) g = atomicAdd(counter, 1u);
     g = __shfl(g, 0);
-    if ((int64_t)g * 64 >= nitems) break;   // wave-uniform: every wave reaches it
-    const int64_t t = (int64_t)g * 64 + lane;
-    const int64_t r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
-    const bool valid = t < nitems && r < nq;
+    if ((int64_t)g * 64 >= items) break;   // wave-uniform: every wave reaches it
+    const int64_t t0 = (int64_t)g * 64 + lane;
+    const bool redo = t0 < nre;             // a retried leader
+    const int64_t t = t0 - nre;
+    int64_t r;
+    if (redo) r = (int64_t)retry[t0];
+    else r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
+    const bool valid = t0 < items && r < nq;
     const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
     const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     const v3 q = {qq.x, qq.y, qq.z};
     float cut = lean_cut(R2);
-    if (valid && !LEADERS) cut = follower_cut(lead, nq, r, q, R2);
+    if (valid && !LEADERS) {
+      if (redo) {   // its own record: the k-th d^2 of a flushed row, if it had one
+        const float ts = lead[r / kSeedStride].w;
+        if (ts >= 0.f) cut = fminf(cut, ts);
+      } else {
+        cut = follower_cut(lead, nq, r, q, R2);
+      }
+    }
     double tail = gkey(cut, kNoWord);
     int cnt = 0;
+    bool aborted = false, flushed = false;
     if (n > 0) {
+      int it_b = 0;   // wave-uniform iterations (leader budget)
       LeanWalk w;
       w.start(cut, valid);
       float4 nd = node1<WIDE>(nodes, 1), ba = bx.box[0], bb = bx.box[1];
@@ -1173,6 +1209,10 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
         const int c0 = cnt;
 #endif
         collect_step<WIDE>(nodes, bx, (uint32_t)n, q, tail, w, nd, ba, bb, row, cnt, stage);
+        if (LEADERS && kWideLeaderBudget > 0 && ++it_b == kWideLeaderBudget) {
+          aborted = w.walking;   // redone at the head of the follower launch
+          w.walking = false;
+        }
         uint64_t full = ballot(cnt == CAP);
         const uint64_t full0 = full;
 #if PM_WIDE_STATS
@@ -1189,6 +1229,7 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
             if (lane == l) {
               cnt = k;
               tail = tl;
+              flushed = true;
               w.bound = gkey_d2(tl);
               if (PM_WIDE_DIAG == 3) w.walking = false;   // diagnostic: an overflowing lane stops
             }
@@ -1197,8 +1238,9 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
           // a full row was flushed chunk by chunk (CAP % 8 == 0); the kept k
           // keys end mid-chunk unless 8 | k: that chunk's head goes back to the
           // stage, so the next chunk write carries it
-          if (PM_WIDE_STAGE && (k & 7) && full0 & (1ull << lane))
-            for (int j = 0; j < (k & 7); j++) stage[j * 256] = row[(k & ~7) + j];
+          constexpr int M = kChunkKeys - 1;
+          if (PM_WIDE_STAGE && (k & M) && full0 & (1ull << lane))
+            for (int j = 0; j < (k & M); j++) stage[j * 256] = row[(k & ~M) + j];
         }
         if (ballot(w.walking) == 0) break;
       }
@@ -1221,7 +1263,7 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
     spill_stage(cnt);
     fence_wave();
 
-    uint64_t live = PM_WIDE_DIAG ? 0 : ballot(cnt > 0);
+    uint64_t live = PM_WIDE_DIAG ? 0 : ballot(cnt > 0 && !aborted);
     while (live) {
       const int l = __ffsll((long long)live) - 1;
       live &= live - 1;
@@ -1234,7 +1276,21 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
       else row_sort<S>(rl, cl, k, lane);
     }
     fence_wave();
-    if (valid) {
+    if (LEADERS && kWideLeaderBudget > 0) {
+      // a leader cut off by the budget: a flushed row's k-th d^2 bounds its k
+      // nearest (any k points do) and seeds its followers and its retry; no
+      // flush yet: nothing. Its own result comes from the retry.
+      if (valid && aborted) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, flushed ? gkey_d2(tail) : -1.f);
+      const uint64_t m = ballot(valid && aborted);
+      if (m != 0) {   // wave-aggregated append to the retry list
+        const int first = __ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == first) base = atomicAdd(nretry, (uint32_t)__popcll(m));
+        base = __shfl(base, first);
+        if (valid && aborted) retry[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint32_t)r;
+      }
+    }
+    if (valid && !aborted) {
       const int m = cnt < k ? cnt : k;
       const bool full = cnt >= k;
       const float r2 = full ? gkey_d2(row[k - 1]) : R2;
@@ -1249,6 +1305,7 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
       const v3 f = divf(flux, (1 - (2.f / 3.f) * (1.f / kConeFilterC)) * 2 * kPI * r2);
       out[i] = make_float4(f.x, f.y, f.z, 0.f);
       if (LEADERS) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, full ? r2 : -1.f);
+      // (a retried leader keeps its soft record: followers may be reading it)
     }
   }
 }
@@ -1275,11 +1332,11 @@ static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb,
     per_cu = 4;
   const int64_t wg = std::min<int64_t>((groups + 3) / 4, (int64_t)device_cus() * per_cu);
   DevBuf<float4> lead(nl);
-  DevBuf<uint32_t> ctr(2);
+  DevBuf<uint32_t> ctr(3), retry(kWideLeaderBudget > 0 ? nl : 1);   // ctr[2]: retried leaders
   DevBuf<double> rows((size_t)wg * 256 * CAP);
   DevBuf<float4> box(2 * (size_t)std::max<int64_t>(boxed_nodes(n, PM_WIDE_BOX_SKIP), 1));
-  if (!lead.p || !ctr.p || !rows.p || !box.p) return hipErrorOutOfMemory;
-  PM_HIP_TRY(hipMemsetAsync(ctr.p, 0, 2 * sizeof(uint32_t), s));
+  if (!lead.p || !ctr.p || !rows.p || !box.p || !retry.p) return hipErrorOutOfMemory;
+  PM_HIP_TRY(hipMemsetAsync(ctr.p, 0, 3 * sizeof(uint32_t), s));
   int64_t nbox = 0;
   PM_HIP_TRY(build_subtree_boxes(m->nodes.p, n, PM_WIDE_BOX_SKIP, box.p, &nbox, s));
   BoxView bx;
@@ -1294,11 +1351,12 @@ static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb,
   const bool wide = PM_FORCE_WIDE || n >= (1 << 28);
 #define PM_WIDE_LAUNCH(W)                                                                                          \
   k_gather_wide<0, true, W, S><<<(int)std::min<int64_t>(wg, (nl + 255) / 256), 256, 0, s>>>(                     \
-      m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p, nl, bx);                              \
+      m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p, nl, bx, retry.p, ctr.p + 2);      \
   PM_HIP_TRY(hipGetLastError());                                                                                 \
-  if (nf > 0) {                                                                                                  \
-    k_gather_wide<0, false, W, S><<<(int)std::min<int64_t>(wg, (nf + 255) / 256), 256, 0, s>>>(                  \
-        m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p + 1, nf, bx);                        \
+  if (nf > 0 || kWideLeaderBudget > 0) {                                                                          \
+    k_gather_wide<0, false, W, S><<<(int)std::min<int64_t>(wg, (nf + nl + 255) / 256), 256, 0, s>>>(             \
+        m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p + 1, nf, bx, retry.p,           \
+        ctr.p + 2);                                                                                              \
     PM_HIP_TRY(hipGetLastError());                                                                               \
   }
   if (wide) {
