@@ -550,6 +550,58 @@ __global__ void k_leaf_place(float4* __restrict__ q, int nn, const uint32_t* __r
   *cp = c4;
 }
 
+// PM_BVH_Q4: the float BVH4 node (8 x float4) -> 64 B (4 x float4, see
+// traverse_step4): corner p = min of the used children's lo, per-axis scale
+// s = 2^e with 255 s >= the children's extent, each child plane rounded
+// outwards (floor / ceil, then stepped until the float decode p + q s encloses
+// the padded float plane), so culling stays conservative and results stay
+// bitwise (argmin (t, id) does not depend on the visit order).
+__global__ void k_quantize4(const float4* __restrict__ f, int nn, float4* __restrict__ q) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nn) return;
+  const float4* fn = f + 8 * (int64_t)i;
+  const float4 lo4[3] = {fn[0], fn[2], fn[4]}, hi4[3] = {fn[1], fn[3], fn[5]};
+  const int4 ch = *reinterpret_cast<const int4*>(&fn[6]);
+  const int cd[4] = {ch.x, ch.y, ch.z, ch.w};
+  auto comp = [](const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); };
+  float p[3];
+  uint32_t eb[3], ql[3] = {0, 0, 0}, qh[3] = {0, 0, 0};
+  for (int a = 0; a < 3; a++) {
+    float lo = INFINITY, hi = -INFINITY;
+    for (int c = 0; c < 4; c++)
+      if (cd[c] != kBvhEmpty) lo = fminf(lo, comp(lo4[a], c)), hi = fmaxf(hi, comp(hi4[a], c));
+    if (!(lo <= hi)) lo = hi = 0.f;   // no used child
+    p[a] = lo;
+    const double ext = (double)hi - (double)lo;
+    int e = 1;
+    if (ext > 0.0) {
+      int k;
+      frexp(ext / 255.0, &k);
+      e = k + 127;
+    }
+    e = e < 1 ? 1 : e;
+    while (e < 254 && q_decode(p[a], 255u, __uint_as_float((uint32_t)e << 23)) < hi) e++;
+    eb[a] = (uint32_t)e;
+    const float sc = __uint_as_float((uint32_t)e << 23);
+    const double inv = 1.0 / (double)sc;
+    for (int c = 0; c < 4; c++) {
+      if (cd[c] == kBvhEmpty) continue;
+      const float bl = comp(lo4[a], c), bh = comp(hi4[a], c);
+      uint32_t l = (uint32_t)fmin(fmax(floor(((double)bl - (double)p[a]) * inv), 0.0), 255.0);
+      uint32_t u = (uint32_t)fmin(fmax(ceil(((double)bh - (double)p[a]) * inv), 0.0), 255.0);
+      while (l > 0 && q_decode(p[a], l, sc) > bl) l--;
+      while (u < 255 && q_decode(p[a], u, sc) < bh) u++;
+      ql[a] |= l << (8 * c);
+      qh[a] |= u << (8 * c);
+    }
+  }
+  float4* qn = q + 4 * (int64_t)i;
+  qn[0] = make_float4(p[0], p[1], p[2], __uint_as_float(eb[0] | eb[1] << 8 | eb[2] << 16));
+  qn[1] = fn[6];
+  qn[2] = make_float4(__uint_as_float(ql[0]), __uint_as_float(ql[1]), __uint_as_float(ql[2]), __uint_as_float(qh[0]));
+  qn[3] = make_float4(__uint_as_float(qh[1]), __uint_as_float(qh[2]), 0.f, 0.f);
+}
+
 static hipError_t collapse_bvh(const float4* bin, int nbin, pm_scene* sc, hipStream_t s) {
   sc->nodes.alloc((size_t)8 * nbin);
   DevBuf<int2> fa(nbin), fb(nbin);
@@ -593,6 +645,15 @@ static hipError_t collapse_bvh(const float4* bin, int nbin, pm_scene* sc, hipStr
     PM_HIP_TRY(hipStreamSynchronize(s));
     std::swap(sc->tri.p, laid.p);
     std::swap(sc->tri.n, laid.n);
+  }
+  if (kBvhQ4) {
+    DevBuf<float4> qn((size_t)4 * alloc);
+    if (!qn.p) return hipErrorOutOfMemory;
+    k_quantize4<<<grid_for(alloc, 256), 256, 0, s>>>(sc->nodes.p, alloc, qn.p);
+    PM_HIP_TRY(hipGetLastError());
+    PM_HIP_TRY(hipStreamSynchronize(s));
+    std::swap(sc->nodes.p, qn.p);
+    std::swap(sc->nodes.n, qn.n);
   }
   return hipSuccess;
 }

@@ -309,6 +309,14 @@ constexpr int kStackDepth = PM_STACK_DEPTH;
 #endif
 constexpr int kBvhWidth = PM_BVH_WIDTH;
 static_assert(kBvhWidth == 4 || kBvhWidth == 8, "PM_BVH_WIDTH is 4 or 8");
+// PM_BVH_Q4 (build knob, width 4): the float BVH4 is converted to 64-B nodes
+// with 8-bit child boxes (bvh.hip, k_quantize4): half the bytes and 4 instead
+// of 7 16-B loads per visited node, for a per-plane fma decode.
+#ifndef PM_BVH_Q4
+#define PM_BVH_Q4 1
+#endif
+constexpr bool kBvhQ4 = PM_BVH_Q4 && kBvhWidth == 4;
+constexpr int kNodeF4 = kBvhQ4 ? 4 : 8;   // float4 per node
 constexpr int kStackTotal = kBvhWidth == 8 ? 128 : 64;
 #ifdef PM_NO_SPILL
 constexpr int kSpillDepth = 0;
@@ -417,12 +425,47 @@ template <bool ANY>
 __device__ __forceinline__ bool traverse_step4(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
                                                int stride, int* spill, int& node, int& sp, HitInfo& h,
                                                int* overflow) {
-  const float4* q = S.nodes + 8 * (int64_t)node;
-  const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
-  const int4 ch = *reinterpret_cast<const int4*>(&q[6]);
   const float lim = (ANY || h.slot < 0) ? tmax * 1.00001f : h.t * 1.00001f;
   float t0, t1, t2, t3;
   bool b0, b1, b2, b3;
+  int4 ch;
+  if (kBvhQ4) {
+    // 64-B node: f4[0] corner p + exponent bytes, f4[1] codes, f4[2] qlo.x qlo.y
+    // qlo.z qhi.x (4 bytes each), f4[3].xy qhi.y qhi.z; plane = p + q * 2^e,
+    // in ray-t space fma(q, 2^e * inv, (p - o) * inv) (conservative: the
+    // decoded box contains the padded float box, as for width 8)
+    const float4* qn = S.nodes + 4 * (int64_t)node;
+    const float4 h0 = qn[0];
+    ch = *reinterpret_cast<const int4*>(&qn[1]);
+    const uint4 qa = *reinterpret_cast<const uint4*>(&qn[2]);
+    const uint2 qb = *reinterpret_cast<const uint2*>(&qn[3]);
+    const uint32_t eb = __float_as_uint(h0.w);
+    const float ax = __uint_as_float((eb & 0xFFu) << 23) * r.inv.x;
+    const float ay = __uint_as_float(((eb >> 8) & 0xFFu) << 23) * r.inv.y;
+    const float az = __uint_as_float(((eb >> 16) & 0xFFu) << 23) * r.inv.z;
+    const float bx = (h0.x - r.o.x) * r.inv.x, by = (h0.y - r.o.y) * r.inv.y, bz = (h0.z - r.o.z) * r.inv.z;
+    float tq[4];
+    bool bq[4];
+    const int cd[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int sh = 8 * c;
+      const float t0x = __builtin_fmaf((float)((qa.x >> sh) & 0xFFu), ax, bx);
+      const float t1x = __builtin_fmaf((float)((qa.w >> sh) & 0xFFu), ax, bx);
+      const float t0y = __builtin_fmaf((float)((qa.y >> sh) & 0xFFu), ay, by);
+      const float t1y = __builtin_fmaf((float)((qb.x >> sh) & 0xFFu), ay, by);
+      const float t0z = __builtin_fmaf((float)((qa.z >> sh) & 0xFFu), az, bz);
+      const float t1z = __builtin_fmaf((float)((qb.y >> sh) & 0xFFu), az, bz);
+      tq[c] = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+      const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), lim));
+      bq[c] = tq[c] <= tf && cd[c] != kBvhEmpty;
+    }
+    t0 = tq[0], t1 = tq[1], t2 = tq[2], t3 = tq[3];
+    b0 = bq[0], b1 = bq[1], b2 = bq[2], b3 = bq[3];
+  } else {
+  const float4* q = S.nodes + 8 * (int64_t)node;
+  const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+  ch = *reinterpret_cast<const int4*>(&q[6]);
   if (PM_SLAB_FMA) {
     const v3 noi = {-r.o.x * r.inv.x, -r.o.y * r.inv.y, -r.o.z * r.inv.z};
     b0 = slab_fma(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, noi, tmin, lim, t0) && ch.x != kBvhEmpty;
@@ -434,6 +477,7 @@ __device__ __forceinline__ bool traverse_step4(const DevScene& S, const Ray& r, 
     b1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tmin, lim, t1) && ch.y != kBvhEmpty;
     b2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tmin, lim, t2) && ch.z != kBvhEmpty;
     b3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tmin, lim, t3) && ch.w != kBvhEmpty;
+  }
   }
   // leaves first: a hit shrinks the limit applied to the internal children
   if (PM_LEAF_BATCH == 4) {

@@ -286,7 +286,7 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths
 // material yields a global-map query (hitpoint, brdf) and its albedo
 // (closestHit + deviceCode.cu:120-129).
 #ifndef PM_RAYS_WAVES
-#define PM_RAYS_WAVES 0   // occupancy target of k_diffuse_rays / k_shadow_rays (0: compiler's choice)
+#define PM_RAYS_WAVES 8   // occupancy target of k_diffuse_rays / k_shadow_rays (0: compiler's choice; 8 with 64-B nodes)
 #endif
 __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_RAYS_WAVES) void k_diffuse_rays(DevScene S, const float4* __restrict__ cq,
                                                           const float4* __restrict__ gdir, int64_t ng,

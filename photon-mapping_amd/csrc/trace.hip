@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void k_ph_gen(const LightDev* __restrict__ lig
 }
 
 #ifndef PM_TPOOL_WAVES
-#define PM_TPOOL_WAVES 0   // occupancy target of k_ph_trace_pool (0: compiler's choice)
+#define PM_TPOOL_WAVES 8   // occupancy target of k_ph_trace_pool (0: compiler's choice; 8 measured best with 64-B nodes)
 #endif
 __global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TPOOL_WAVES) void k_ph_trace_pool(
     DevScene S, const PhotonRay* __restrict__ rays, const uint32_t* __restrict__ live, float2* __restrict__ hits,
