@@ -554,8 +554,83 @@ constexpr int kLocal = 1024;
 constexpr int kLocalWaveLevel = 4;
 static_assert(kLocal / 64 == (1 << kLocalWaveLevel), "one wave per level-4 sub-segment");
 
-__global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_kd_local(KdLists Lst, int L0,
-                                                                                           SegTab T,
+// The selection build's elements: four SoA arrays (x, y, z, index bits) per
+// buffer k (0 / 1), unsorted inside each subtree range.
+struct KdSoa {
+  float* base;
+  int64_t n;
+  __host__ __device__ float* comp(int k, int c) const { return base + (int64_t)(k * 4 + c) * n; }
+};
+
+// lane ^ stride exchange for stride < 64: DPP quad permutes for 1 and 2 (VALU),
+// ds_swizzle's xor mode for 4 .. 16, ds_bpermute for 32
+__device__ __forceinline__ int xor_lane(int v, int stride) {
+  switch (stride) {
+    case 1: return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1, 0, 3, 2]
+    case 2: return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2, 3, 0, 1]
+    case 4: return __builtin_amdgcn_ds_swizzle(v, 0x1F | (4 << 10));
+    case 8: return __builtin_amdgcn_ds_swizzle(v, 0x1F | (8 << 10));
+    case 16: return __builtin_amdgcn_ds_swizzle(v, 0x1F | (16 << 10));
+    default: return __shfl_xor(v, stride);
+  }
+}
+
+// min / max over the 64 lanes of a wave, valid in every lane: DPP row shifts
+// inside each 16-lane row (identity shifted in), then the four row results
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_minmax(uint32_t v) {
+  const int id = MAX ? 0 : (int)0xFFFFFFFFu;
+  auto op = [](uint32_t a, uint32_t b) { return MAX ? max(a, b) : min(a, b); };
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x111, 0xF, 0xF, false));   // row_shr:1
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x112, 0xF, 0xF, false));   // row_shr:2
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x114, 0xF, 0xF, false));   // row_shr:4
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x118, 0xF, 0xF, false));   // row_shr:8
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 15), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 47), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  return op(op(a, b), op(c, d));
+}
+
+// Block-wide bitonic sort (blockDim = kLocal, one (key, slot) pair per thread,
+// ascending over the first n2 threads, n2 a power of two >= 64): strides below
+// 64 exchange through wave shuffles, larger ones through LDS (kx / vx).
+__device__ __forceinline__ void block_bitonic(uint64_t& k, int& v, int n2, uint64_t* kx, int16_t* vx) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int ls = 1; ls <= 10; ls++) {   // size 2 .. 1024, every stride a constant after unrolling
+    const int size = 1 << ls;
+#pragma unroll
+    for (int lst = ls - 1; lst >= 0; lst--) {
+      if (size > n2) continue;   // n2 is uniform: the barriers below are reached by all or none
+      const int stride = 1 << lst;
+      uint64_t pk;
+      int pv;
+      if (stride >= 64) {
+        __syncthreads();   // the previous stage's reads are done
+        kx[tid] = k;
+        vx[tid] = (int16_t)v;
+        __syncthreads();
+        pk = kx[tid ^ stride];
+        pv = vx[tid ^ stride];
+      } else {
+        pk = (uint64_t)(uint32_t)xor_lane((int)(uint32_t)k, stride) |
+             (uint64_t)(uint32_t)xor_lane((int)(uint32_t)(k >> 32), stride) << 32;
+        pv = xor_lane(v, stride);
+      }
+      const bool up = (tid & size) == 0, lower = (tid & stride) == 0;
+      if (lower == up ? pk < k : pk > k) {
+        k = pk;
+        v = pv;
+      }
+    }
+  }
+}
+
+// SORT (the selection build): the subtree's elements arrive unsorted in E; the
+// three lists are made in LDS by sorting (orderable coordinate, index) keys,
+// the presort's order. Otherwise they are loaded from the presorted lists.
+template <bool SORT>
+__global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_kd_local(KdLists Lst, KdSoa E,
+                                                                                           int L0, SegTab T,
                                                                                            float4* __restrict__ nodes) {
   __shared__ float4 buf[3][kLocal];
   __shared__ int16_t tag[kLocal];
@@ -571,10 +646,33 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
   const int64_t t = ((int64_t)1 << L0) - 1 + blockIdx.x;
   const int B = T.b[t], S = T.s[t];
   if (S <= 0) return;
-  const int sel = T.sel[t];
-  if (tid < S) {
+  if (SORT) {
+    const int k0 = L0 & 1;
+    float4 me = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < S) {
+      me = make_float4(E.comp(k0, 0)[B + tid], E.comp(k0, 1)[B + tid], E.comp(k0, 2)[B + tid], E.comp(k0, 3)[B + tid]);
+      buf[2][tid] = me;
+    }
+    int n2 = 64;
+    while (n2 < S) n2 <<= 1;
+    uint64_t* kx = reinterpret_cast<uint64_t*>(stage);   // scratch until stage is set below
+#pragma unroll 1
+    for (int d = 0; d < 3; d++) {
+      uint64_t k = tid < S ? (uint64_t)orderable_key(coord_of(me, d)) << 32 | (uint32_t)__float_as_int(me.w) : ~0ull;
+      int v = tid;
+      block_bitonic(k, v, n2, kx, tag);
+      __syncthreads();   // buf[2] written; every exchange read
+      const float4 x = tid < S ? buf[2][v] : me;
+      if (d == 2) __syncthreads();
+      if (tid < S) buf[d][tid] = x;
+    }
+    __syncthreads();
+  } else {
+    const int sel = T.sel[t];
+    if (tid < S) {
 #pragma unroll
-    for (int d = 0; d < 3; d++) buf[d][tid] = kd_elem(Lst, d, (sel >> d) & 1, B + tid);
+      for (int d = 0; d < 3; d++) buf[d][tid] = kd_elem(Lst, d, (sel >> d) & 1, B + tid);
+    }
   }
   tag[tid] = tid < S ? 0 : -1;
   stage[tid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
@@ -742,7 +840,925 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
   }
 }
 
+// ------------------------------------------------------------------ selection build
+// The production build (round 3): no presort. The elements stay unsorted in
+// their subtree ranges (SoA, ping-pong by level) and every global level
+//   k_ks_seg      picks each subtree's split dimension from its extents (the
+//                 orderable-key min / max of its elements, reduced by the
+//                 previous level's partition) -- the same float extents the
+//                 presorted lists give (first and last element);
+//   k_ks_hist / k_ks_find / k_ks_compact / k_ks_cand
+//                 select the element of rank left_size(s) in (coordinate,
+//                 index) order: a 256-bin histogram of the coordinate scaled to
+//                 the subtree's range (monotone in the coordinate, so equal
+//                 coordinates share a bin and bins follow the order), the bin
+//                 holding the rank, a compaction of that bin's elements into
+//                 the subtree's own range of a candidate buffer as the unique
+//                 keys K = (orderable(coord) - min) << idbits | index, and one
+//                 workgroup per subtree that radix-selects among them (8-bit
+//                 digits while more than 256 match, then a sort in LDS);
+//   k_ks_part     moves every element to its child range (unstable: one atomic
+//                 per wave and (subtree, side) reserves slots; the order inside
+//                 a range does not matter, the median is defined by rank) and
+//                 reduces the children's extents.
+// Per element and level: 4 B (histogram) + 4 B (compaction) + 16 B read and
+// 16 B written (partition), against the presorted build's 72 B plus its
+// 12-pass presort. Once subtrees hold <= 1023 elements, k_kd_local<true> sorts
+// each one's three lists in LDS and finishes it like the presorted build.
+// Same medians, same tree: the check variant keeps the presorted build, and
+// tests/test_gpu_check_variant.py compares the two bit for bit.
+#ifndef PM_KS_IPT
+#define PM_KS_IPT 8   // positions per thread of the per-position selection kernels
+#endif
+#ifndef PM_KS_NSUB
+#define PM_KS_NSUB 4   // sub-tiles per block (one subtree prologue for all of them)
+#endif
+constexpr int kSelThreads = 256;
+constexpr int kSelIPT = PM_KS_IPT;
+constexpr int kSelTile = kSelThreads * kSelIPT;   // positions per sub-tile
+constexpr int kSelNSub = PM_KS_NSUB;
+constexpr int kSelBlock = kSelTile * kSelNSub;    // positions per block
+constexpr int kSelCache = 4 + 2 * kSelNSub;       // subtrees staged per block (global-level subtrees hold >= 1023)
+constexpr int kCandThreads = 256;                  // k_ks_cand: LDS sort of <= 256 keys
+#ifndef PM_KS_CANDCAP
+#define PM_KS_CANDCAP 65536
+#endif
+constexpr int kCandCap = PM_KS_CANDCAP;            // larger candidate sets: grid-wide radix passes first
+
+struct SelTab {
+  uint32_t* ext[2];   // per subtree: orderable min x, y, z, max x, y, z (by level parity)
+  int32_t* dim;       // split dimension (-1: empty subtree)
+  uint32_t* kmin;     // orderable min along dim
+  float* vlo;         // first pass: bin = (coord - vlo) * vsc, clamped to 0 .. 255
+  float* vsc;
+  int32_t* vbin;      // the bin holding the median
+  uint32_t* rank;     // the median's rank (inside vbin after k_ks_find)
+  int32_t* tb;        // key bits
+  uint64_t* med;      // the median's key
+  uint32_t* hist;     // 256 bins per subtree
+  uint32_t* cnt;      // partition slots taken: left, right per subtree
+  uint32_t* ccnt;     // candidates per subtree
+  uint64_t* cand;     // candidate keys, subtree j's at [b_j, b_j + ccnt_j)
+  uint64_t* cmin;     // range of the subtree's candidate keys
+  uint64_t* cmax;
+  int32_t* cshift;    // candidate radix select: key bits still to select,
+  uint64_t* cprefix;  //   the selected bits above them,
+  uint32_t* cmatch;   //   and how many candidates carry them
+  uint64_t* cand2;    // large sets: the keys left after the grid passes, at [b_j, b_j + cnt2_j)
+  uint32_t* cnt2;
+  int idbits;
+};
+
+__device__ __forceinline__ float key_float(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+__device__ __forceinline__ int bitlen32(uint32_t x) { return x ? 32 - __clz((int)x) : 0; }
+// monotone non-decreasing in c (float subtraction and scaling round
+// monotonically; NaN from inf * 0 lands in bin 0 with everything else)
+__device__ __forceinline__ int vbin_of(float c, float lo, float sc) {
+  const float t = (c - lo) * sc;
+  return t >= 255.f ? 255 : (t > 0.f ? (int)t : 0);
+}
+
+// The bin of a 256-bin histogram (4 bins per lane of one wave) that holds
+// rank `rank`: returns false if none does; r = the rank inside the bin, cb =
+// its count.
+__device__ __forceinline__ bool wave_pick_bin(uint4 c4, uint32_t rank, int& bin, uint32_t& r, uint32_t& cb) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t sum = c4.x + c4.y + c4.z + c4.w;
+  uint32_t inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t up = (uint32_t)__shfl_up((int)inc, o);
+    if (lane >= o) inc += up;
+  }
+  const uint32_t ex = inc - sum;
+  const uint64_t hit = __ballot(ex <= rank && rank < inc);
+  if (!hit || lane != __ffsll((unsigned long long)hit) - 1) return false;
+  r = rank - ex;
+  bin = 0;
+  cb = c4.x;
+  if (r >= c4.x) {
+    r -= c4.x;
+    bin = 1;
+    cb = c4.y;
+    if (r >= c4.y) {
+      r -= c4.y;
+      bin = 2;
+      cb = c4.z;
+      if (r >= c4.z) {
+        r -= c4.z;
+        bin = 3;
+        cb = c4.w;
+      }
+    }
+  }
+  bin += 4 * lane;
+  return true;
+}
+
+// root: elements -> SoA buffer 0, extents of the whole set (one atomic per wave)
+constexpr int kInitBlocks = 2048;   // grid-stride: few blocks, few same-address atomics
+__global__ __launch_bounds__(256) void k_ks_init(const float4* __restrict__ elems, int64_t n, KdSoa E,
+                                                 uint32_t* __restrict__ ext) {
+  uint32_t mn[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, mx[3] = {0u, 0u, 0u};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)kInitBlocks * 256) {
+    const float4 e = elems[i];
+    E.comp(0, 0)[i] = e.x;
+    E.comp(0, 1)[i] = e.y;
+    E.comp(0, 2)[i] = e.z;
+    E.comp(0, 3)[i] = e.w;
+    const float c[3] = {e.x, e.y, e.z};
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const uint32_t kk = orderable_key(c[d]);
+      mn[d] = min(mn[d], kk);
+      mx[d] = max(mx[d], kk);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mn[d] = min(mn[d], (uint32_t)__shfl_xor((int)mn[d], o));
+      mx[d] = max(mx[d], (uint32_t)__shfl_xor((int)mx[d], o));
+    }
+  }
+  __shared__ uint32_t wmn[4][3], wmx[4][3];   // blockDim = 256
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) wmn[w][d] = mn[d], wmx[w][d] = mx[d];
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {   // one atomic per block and component
+    const int d = threadIdx.x;
+    const uint32_t a = min(min(wmn[0][d], wmn[1][d]), min(wmn[2][d], wmn[3][d]));
+    const uint32_t b = max(max(wmx[0][d], wmx[1][d]), max(wmx[2][d], wmx[3][d]));
+    atomicMin(&ext[d], a);
+    atomicMax(&ext[3 + d], b);
+  }
+}
+
+// per subtree of level L: split dimension, selection state, children ranges,
+// the children's extent accumulators and the counters reset
+__global__ void k_ks_seg(int level, int64_t cap, SegTab T, SelTab S) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nseg = 1ll << level;
+  if (j >= nseg) return;
+  const int64_t t = nseg - 1 + j;
+  const int b = T.b[t], s = T.s[t];
+  const int64_t c1 = 2 * t + 1, c2 = 2 * t + 2;
+  uint32_t* nx = S.ext[(level + 1) & 1];
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      nx[(2 * j + c) * 6 + d] = 0xFFFFFFFFu;
+      nx[(2 * j + c) * 6 + 3 + d] = 0u;
+    }
+    S.cnt[2 * j + c] = 0;
+  }
+  S.ccnt[j] = 0;
+  S.cmin[j] = ~0ull;
+  S.cmax[j] = 0ull;
+  S.cnt2[j] = 0;
+  if (s <= 0) {
+    S.dim[j] = -1;
+    T.ls[t] = -1;
+    if (c2 < cap) {
+      T.b[c1] = b; T.s[c1] = 0;
+      T.b[c2] = b; T.s[c2] = 0;
+    }
+    return;
+  }
+  const int ls = left_size(s);
+  const uint32_t* ex = S.ext[level & 1] + j * 6;
+  float ext[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) ext[d] = key_float(ex[3 + d]) - key_float(ex[d]);
+  int dim = 0;
+  if (ext[1] > ext[dim]) dim = 1;
+  if (ext[2] > ext[dim]) dim = 2;
+  const float lo = key_float(ex[dim]), range = ext[dim];
+  S.dim[j] = dim;
+  S.kmin[j] = ex[dim];
+  S.vlo[j] = lo;
+  S.vsc[j] = range > 0.f ? 256.f / range : 0.f;   // inf range: 0 (one bin)
+  S.tb[j] = bitlen32(ex[3 + dim] - ex[dim]) + S.idbits;
+  S.rank[j] = (uint32_t)ls;
+  T.ls[t] = ls;
+  T.dim[t] = dim;
+  if (c2 < cap) {
+    T.b[c1] = b; T.s[c1] = ls;
+    T.b[c2] = b + ls + 1; T.s[c2] = s - ls - 1;
+  }
+}
+
+// a subtree as the per-position kernels see it
+struct SelRec {
+  int b, s, dim, vbin;
+  uint32_t kmin;
+  float vlo, vsc;
+  uint64_t med;
+  int cb[2];   // children starts (k_ks_part)
+};
+
+__device__ __forceinline__ SelRec sel_load(const SegTab& T, const SelTab& S, int level, int j, bool med) {
+  const int64_t t = (1ll << level) - 1 + j;
+  SelRec r;
+  r.b = T.b[t];
+  r.s = T.s[t];
+  r.dim = S.dim[j];
+  r.kmin = S.kmin[j];
+  r.vlo = S.vlo[j];
+  r.vsc = S.vsc[j];
+  r.vbin = S.vbin[j];
+  r.med = med ? S.med[j] : 0ull;
+  r.cb[0] = med ? T.b[2 * t + 1] : 0;
+  r.cb[1] = med ? T.b[2 * t + 2] : 0;
+  return r;
+}
+
+// slot (j - jl) of position p in a cached tile, -1: a placed median / past n
+__device__ __forceinline__ int sel_slot(const SelRec* cache, int nslot, int64_t p) {
+  int k = 0;
+  for (int c = 1; c < nslot; c++)
+    if ((int64_t)cache[c].b <= p) k = c;
+  const SelRec& r = cache[k];
+  return (r.s > 0 && p >= r.b && p < (int64_t)r.b + r.s) ? k : -1;
+}
+
+// the subtrees a kSelTile-position block can meet: jl .. jh (tile_seg);
+// staged in LDS when there are few (always, in practice: global-level subtrees
+// hold >= 1023 elements)
+struct SelTile {
+  int jl, jh;
+  bool cached;
+};
+
+__device__ __forceinline__ SelTile sel_tile(const SegTab& T, const SelTab& S, int level, bool med,
+                                            const int32_t* __restrict__ tile_seg, SelRec* cache) {
+  SelTile st;
+  st.jl = tile_seg[blockIdx.x];
+  st.jh = tile_seg[blockIdx.x + 1];
+  st.cached = st.jh - st.jl < kSelCache;
+  if (st.cached)
+    for (int j = st.jl + (int)threadIdx.x; j <= st.jh; j += blockDim.x)
+      cache[j - st.jl] = sel_load(T, S, level, j, med);
+  __syncthreads();
+  return st;
+}
+
+// subtree of position p (-1: a placed median / outside every subtree)
+__device__ __forceinline__ int sel_find(const SegTab& T, const SelTab& S, int level, bool med, const SelTile& st,
+                                        const SelRec* cache, int64_t p, SelRec& r) {
+  int j;
+  if (st.cached) {
+    int k = 0;
+    for (int c = 1; c <= st.jh - st.jl; c++)
+      if ((int64_t)cache[c].b <= p) k = c;
+    r = cache[k];
+    j = st.jl + k;
+  } else {
+    const int64_t base = (1ll << level) - 1;
+    int lo = st.jl, hi = st.jh + 1;
+    while (hi - lo > 1) {
+      const int m = (lo + hi) >> 1;
+      if ((int64_t)T.b[base + m] <= p) lo = m;
+      else hi = m;
+    }
+    r = sel_load(T, S, level, lo, med);
+    j = lo;
+  }
+  return (r.s > 0 && p >= r.b && p < (int64_t)r.b + r.s) ? j : -1;
+}
+
+// k_kd_tileseg for a runtime tile size
+__global__ void k_kd_tileseg_n(const int32_t* __restrict__ tb, int level, int64_t ntiles, int tile,
+                               int32_t* __restrict__ tile_seg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > ntiles) return;
+  const int64_t base = (1ll << level) - 1, nseg = 1ll << level;
+  const int64_t p = i < ntiles ? i * tile : INT64_MAX;
+  int64_t lo = 0, hi = nseg;
+  while (hi - lo > 1) {
+    const int64_t m = (lo + hi) >> 1;
+    if ((int64_t)tb[base + m] <= p) lo = m;
+    else hi = m;
+  }
+  tile_seg[i] = (int32_t)lo;
+}
+
+// (slot, bin) groups of a wave merged before the atomic: up to `rounds` leader
+// rounds, then one atomic per remaining lane
+__device__ __forceinline__ void merged_add(uint32_t* base, int key, int rounds) {
+  const int lane = threadIdx.x & 63;
+  uint64_t todo = __ballot(key >= 0);
+  for (int r = 0; todo && r < rounds; r++) {
+    const int l = __ffsll((unsigned long long)todo) - 1;
+    const int kl = __shfl(key, l);
+    const uint64_t same = __ballot(key == kl) & todo;
+    if (lane == l) atomicAdd(&base[kl], (uint32_t)__popcll(same));
+    if ((same >> lane) & 1) key = -1;
+    todo &= ~same;
+  }
+  if (key >= 0) atomicAdd(&base[key], 1u);
+}
+
+// first selection pass: 256-bin histograms of the scaled coordinate, per
+// block in LDS, flushed with one atomic per used bin. Every item's load is
+// issued before any is used (the per-item atomics would otherwise serialise
+// the loads behind them).
+__global__ __launch_bounds__(kSelThreads) void k_ks_hist(KdSoa E, int64_t n, SegTab T, SelTab S, int level,
+                                                         const int32_t* __restrict__ tile_seg) {
+  __shared__ SelRec cache[kSelCache];
+  __shared__ uint32_t lh[kSelCache * 256];
+  const SelTile st = sel_tile(T, S, level, false, tile_seg, cache);
+  const int k = level & 1;
+  const int64_t t0 = (int64_t)blockIdx.x * kSelBlock;
+  if (!st.cached) {   // never at global levels (subtrees of >= 1023 elements); kept general
+    for (int it = 0; it < kSelIPT * kSelNSub; it++) {
+      const int64_t p = t0 + it * kSelThreads + threadIdx.x;
+      SelRec r;
+      const int j = p < n ? sel_find(T, S, level, false, st, cache, p, r) : -1;
+      if (j >= 0) atomicAdd(&S.hist[(int64_t)j * 256 + vbin_of(E.comp(k, r.dim)[p], r.vlo, r.vsc)], 1u);
+    }
+    return;
+  }
+  const int nslot = st.jh - st.jl + 1;
+  for (int i = threadIdx.x; i < nslot * 256; i += kSelThreads) lh[i] = 0;
+  __syncthreads();
+  for (int sub = 0; sub < kSelNSub; sub++) {
+    const int64_t ts = t0 + (int64_t)sub * kSelTile;
+    int sl[kSelIPT];
+    float cv[kSelIPT];
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {
+      const int64_t p = ts + it * kSelThreads + threadIdx.x;
+      sl[it] = p < n ? sel_slot(cache, nslot, p) : -1;
+    }
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {   // every load issued before any is used
+      const int64_t p = ts + it * kSelThreads + threadIdx.x;
+      cv[it] = E.comp(k, cache[sl[it] < 0 ? 0 : sl[it]].dim)[sl[it] < 0 ? 0 : p];
+    }
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {
+      int key = -1;
+      if (sl[it] >= 0) {
+        const SelRec& r = cache[sl[it]];
+        key = sl[it] * 256 + vbin_of(cv[it], r.vlo, r.vsc);
+      }
+      merged_add(lh, key, 2);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nslot * 256; i += kSelThreads) {
+    const uint32_t c = lh[i];
+    if (c) atomicAdd(&S.hist[(int64_t)st.jl * 256 + i], c);
+  }
+}
+
+// one wave per subtree: the bin holding the median's rank (its rank inside
+// the bin kept); the bins are cleared for the next use
+__global__ __launch_bounds__(64) void k_ks_find(SelTab S) {
+  const int j = blockIdx.x, lane = threadIdx.x;
+  if (S.dim[j] < 0) return;
+  uint32_t* h = S.hist + (int64_t)j * 256;
+  const uint4 c4 = reinterpret_cast<const uint4*>(h)[lane];
+  reinterpret_cast<uint4*>(h)[lane] = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t r, cb;
+  int bin;
+  if (!wave_pick_bin(c4, S.rank[j], bin, r, cb)) return;
+  S.vbin[j] = bin;
+  S.rank[j] = r;
+}
+
+// the median bin's elements -> the subtree's candidate range, as keys, with
+// the range of those keys (per block in LDS, one atomic per block and subtree)
+__global__ __launch_bounds__(kSelThreads) void k_ks_compact(KdSoa E, int64_t n, SegTab T, SelTab S, int level,
+                                                            const int32_t* __restrict__ tile_seg) {
+  __shared__ SelRec cache[kSelCache];
+  __shared__ uint32_t lcc[kSelCache], lbase[kSelCache];
+  __shared__ unsigned long long lkmin[kSelCache], lkmax[kSelCache];
+  const SelTile st = sel_tile(T, S, level, false, tile_seg, cache);
+  const int k = level & 1;
+  const int lane = threadIdx.x & 63;
+  const int64_t t0 = (int64_t)blockIdx.x * kSelBlock;
+  if (!st.cached) {   // never at global levels; kept general
+    for (int it = 0; it < kSelIPT * kSelNSub; it++) {
+      const int64_t p = t0 + it * kSelThreads + threadIdx.x;
+      SelRec r;
+      const int j = p < n ? sel_find(T, S, level, false, st, cache, p, r) : -1;
+      if (j < 0) continue;
+      const float c = E.comp(k, r.dim)[p];
+      if (vbin_of(c, r.vlo, r.vsc) != r.vbin) continue;
+      const uint64_t key = (uint64_t)(orderable_key(c) - r.kmin) << S.idbits | (uint32_t)__float_as_int(E.comp(k, 3)[p]);
+      S.cand[(int64_t)r.b + atomicAdd(&S.ccnt[j], 1u)] = key;
+      atomicMin((unsigned long long*)&S.cmin[j], (unsigned long long)key);
+      atomicMax((unsigned long long*)&S.cmax[j], (unsigned long long)key);
+    }
+    return;
+  }
+  const int nslot = st.jh - st.jl + 1;
+  if (threadIdx.x < nslot) {
+    lkmin[threadIdx.x] = ~0ull;
+    lkmax[threadIdx.x] = 0ull;
+  }
+  for (int sub = 0; sub < kSelNSub; sub++) {
+    const int64_t ts = t0 + (int64_t)sub * kSelTile;
+    if (threadIdx.x < nslot) lcc[threadIdx.x] = 0;
+    int sl[kSelIPT];
+    float cv[kSelIPT];
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {
+      const int64_t p = ts + it * kSelThreads + threadIdx.x;
+      sl[it] = p < n ? sel_slot(cache, nslot, p) : -1;
+    }
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {
+      const int64_t p = ts + it * kSelThreads + threadIdx.x;
+      cv[it] = E.comp(k, cache[sl[it] < 0 ? 0 : sl[it]].dim)[sl[it] < 0 ? 0 : p];
+    }
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++)
+      if (sl[it] >= 0 && vbin_of(cv[it], cache[sl[it]].vlo, cache[sl[it]].vsc) != cache[sl[it]].vbin) sl[it] = -1;
+    uint32_t idv[kSelIPT];
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {
+      const int64_t p = ts + it * kSelThreads + threadIdx.x;
+      idv[it] = sl[it] >= 0 ? (uint32_t)__float_as_int(E.comp(k, 3)[p]) : 0u;
+    }
+    __syncthreads();   // lcc reset (and the previous sub-tile's lbase reads) done
+    uint64_t key[kSelIPT];
+    uint32_t rk[kSelIPT];
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {
+      const int g = sl[it];
+      key[it] = g >= 0 ? (uint64_t)(orderable_key(cv[it]) - cache[g].kmin) << S.idbits | idv[it] : 0ull;
+      rk[it] = 0;
+      uint64_t todo = __ballot(g >= 0);
+      while (todo) {
+        const int l = __ffsll((unsigned long long)todo) - 1;
+        const int gl = __shfl(g, l);
+        const uint64_t same = __ballot(g == gl) & todo;
+        const bool in = (same >> lane) & 1;
+        unsigned long long mn = in ? key[it] : ~0ull, mx = in ? key[it] : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          mn = min(mn, (unsigned long long)__shfl_xor(mn, o));
+          mx = max(mx, (unsigned long long)__shfl_xor(mx, o));
+        }
+        uint32_t base = 0;
+        if (lane == l) {
+          base = atomicAdd(&lcc[gl], (uint32_t)__popcll(same));
+          atomicMin(&lkmin[gl], mn);
+          atomicMax(&lkmax[gl], mx);
+        }
+        base = (uint32_t)__shfl((int)base, l);
+        if (in) rk[it] = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+        todo &= ~same;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < nslot) {
+      const uint32_t c = lcc[threadIdx.x];
+      lbase[threadIdx.x] = c ? atomicAdd(&S.ccnt[st.jl + threadIdx.x], c) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++)
+      if (sl[it] >= 0) S.cand[(int64_t)cache[sl[it]].b + lbase[sl[it]] + rk[it]] = key[it];
+  }
+  if (threadIdx.x < nslot && lkmin[threadIdx.x] <= lkmax[threadIdx.x]) {
+    const int j = st.jl + threadIdx.x;
+    atomicMin((unsigned long long*)&S.cmin[j], lkmin[threadIdx.x]);
+    atomicMax((unsigned long long*)&S.cmax[j], lkmax[threadIdx.x]);
+  }
+}
+
+// candidate selection state: the digits above the highest bit in which the
+// subtree's candidate keys differ are common to all of them
+__global__ void k_ks_cinit(int64_t nseg, SelTab S) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nseg || S.dim[j] < 0) return;
+  const uint64_t a = S.cmin[j], b = S.cmax[j];
+  const int sh = (a ^ b) ? 64 - __clzll((long long)(a ^ b)) : 0;
+  S.cshift[j] = sh;
+  S.cprefix[j] = sh >= 64 ? 0ull : a >> sh;
+  S.cmatch[j] = S.ccnt[j];
+}
+
+// a radix pass over a large candidate set, spread over gridDim.x blocks per
+// subtree (subtrees with <= kCandCap matching keys are left to k_ks_cand)
+__global__ __launch_bounds__(kSelThreads) void k_ks_chist(int level, SegTab T, SelTab S) {
+  __shared__ uint32_t h[256];
+  const int j = blockIdx.y;
+  if (S.dim[j] < 0) return;
+  const int shift = S.cshift[j];
+  if (S.cmatch[j] <= (uint32_t)kCandCap || shift <= 0) return;
+  const uint64_t prefix = S.cprefix[j];
+  const int w = min(8, shift);
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t total = S.ccnt[j];
+  const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
+  const uint32_t lo = blockIdx.x * per, hi = min(total, lo + per);
+  const uint64_t* cand = S.cand + T.b[(1ll << level) - 1 + j];
+  for (uint32_t i0 = lo; i0 < hi; i0 += kSelThreads) {
+    const uint32_t i = i0 + threadIdx.x;
+    int bin = -1;
+    if (i < hi) {
+      const uint64_t key = cand[i];
+      if ((key >> shift) == prefix) bin = (int)((key >> (shift - w)) & ((1u << w) - 1u));
+    }
+    merged_add(h, bin, 2);
+  }
+  __syncthreads();
+  const uint32_t c = h[threadIdx.x];
+  if (c) atomicAdd(&S.hist[(int64_t)j * 256 + threadIdx.x], c);
+}
+
+__global__ __launch_bounds__(64) void k_ks_cfind(SelTab S) {
+  const int j = blockIdx.x;
+  if (S.dim[j] < 0) return;
+  const int shift = S.cshift[j];
+  if (S.cmatch[j] <= (uint32_t)kCandCap || shift <= 0) return;
+  uint32_t* h = S.hist + (int64_t)j * 256;
+  const uint4 c4 = reinterpret_cast<const uint4*>(h)[threadIdx.x];
+  reinterpret_cast<uint4*>(h)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t r, cb;
+  int bin;
+  if (!wave_pick_bin(c4, S.rank[j], bin, r, cb)) return;
+  const int w = min(8, shift);
+  S.cprefix[j] = S.cprefix[j] << w | (uint64_t)bin;
+  S.cshift[j] = shift - w;
+  S.rank[j] = r;
+  S.cmatch[j] = cb;
+}
+
+// large sets after the grid passes: the keys still matching -> cand2 (one
+// atomic per wave)
+__global__ __launch_bounds__(kSelThreads) void k_ks_cgather(int level, SegTab T, SelTab S) {
+  const int j = blockIdx.y, lane = threadIdx.x & 63;
+  if (S.dim[j] < 0 || S.ccnt[j] <= (uint32_t)kCandCap) return;
+  const int shift = S.cshift[j];
+  const uint64_t prefix = S.cprefix[j];
+  const uint32_t total = S.ccnt[j];
+  const uint32_t per = (total + gridDim.x - 1) / gridDim.x;
+  const uint32_t lo = blockIdx.x * per, hi = min(total, lo + per);
+  const int64_t b = T.b[(1ll << level) - 1 + j];
+  const uint64_t* cand = S.cand + b;
+  for (uint32_t i0 = lo; i0 < hi; i0 += kSelThreads) {
+    const uint32_t i = i0 + threadIdx.x;
+    uint64_t key = 0;
+    bool take = false;
+    if (i < hi) {
+      key = cand[i];
+      take = (key >> shift) == prefix;
+    }
+    const uint64_t m = __ballot(take);
+    if (!m) continue;
+    const int l = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == l) base = atomicAdd(&S.cnt2[j], (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, l);
+    if (take) S.cand2[b + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = key;
+  }
+}
+
+// one workgroup per subtree: the candidate of the median's rank. While more
+// than kCandThreads keys match the selected prefix, an 8-bit radix pass over
+// them (LDS histogram); then the matching keys are sorted in LDS. Writes the
+// median's key and its node (position from elems[index]).
+__global__ __launch_bounds__(kCandThreads) void k_ks_cand(int level, SegTab T, SelTab S,
+                                                          const float4* __restrict__ elems,
+                                                          float4* __restrict__ nodes, bool gathered) {
+  __shared__ uint32_t h[256];
+  __shared__ uint64_t lk[kCandThreads], kx[kCandThreads];
+  __shared__ int16_t vx[kCandThreads];
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_rank, s_cnt;
+  __shared__ int s_shift;
+  const int j = blockIdx.x, tid = threadIdx.x;
+  if (S.dim[j] < 0) return;
+  const int64_t t = (1ll << level) - 1 + j;
+  const bool big = gathered && S.ccnt[j] > (uint32_t)kCandCap;   // k_ks_cgather ran for it
+  const uint64_t* cand = (big ? S.cand2 : S.cand) + T.b[t];
+  const uint32_t total = big ? S.cnt2[j] : S.ccnt[j];
+  uint32_t rank = S.rank[j], c = S.cmatch[j];
+  uint64_t prefix = S.cprefix[j];
+  int shift = S.cshift[j];
+  while (c > kCandThreads && shift > 0) {   // keys are unique: c == 1 once shift == 0
+    const int w = min(8, shift);
+    h[tid] = 0;
+    if (tid == 0) {   // a rank outside the histogram ends the loop (never, with consistent counts)
+      s_prefix = prefix;
+      s_rank = rank;
+      s_cnt = 0;
+      s_shift = 0;
+    }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < total; i0 += kCandThreads) {
+      const uint32_t i = i0 + tid;
+      int bin = -1;
+      if (i < total) {
+        const uint64_t key = cand[i];
+        if ((key >> shift) == prefix) bin = (int)((key >> (shift - w)) & ((1u << w) - 1u));
+      }
+      merged_add(h, bin, 2);
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const uint4 c4 = reinterpret_cast<const uint4*>(h)[tid];
+      uint32_t r, cb;
+      int bin;
+      if (wave_pick_bin(c4, rank, bin, r, cb)) {
+        s_prefix = prefix << w | (uint64_t)bin;
+        s_rank = r;
+        s_cnt = cb;
+        s_shift = shift - w;
+      }
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    rank = s_rank;
+    c = s_cnt;
+    shift = s_shift;
+    __syncthreads();
+  }
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < total; i += kCandThreads) {
+    const uint64_t key = cand[i];
+    if ((key >> shift) == prefix) {
+      const uint32_t o = atomicAdd(&s_cnt, 1u);
+      if (o < kCandThreads) lk[o] = key;
+    }
+  }
+  __syncthreads();
+  c = min(s_cnt, (uint32_t)kCandThreads);
+  int n2 = 64;
+  while (n2 < (int)c) n2 <<= 1;
+  uint64_t key = tid < (int)c ? lk[tid] : ~0ull;
+  int v = tid;
+  block_bitonic(key, v, n2, kx, vx);
+  if (tid == (int)rank) {
+    S.med[j] = key;
+    const int id = (int)(key & ((1ull << S.idbits) - 1ull));
+    const int dim = S.dim[j];
+    const float4 e = elems[id];
+    T.id[t] = id;
+    T.coord[t] = coord_of(e, dim);
+    nodes[t] = make_float4(e.x, e.y, e.z, __int_as_float((id << 2) | dim));
+  }
+}
+
+// every element to its child range; the children's extents reduced per lane
+// (the block's first two subtrees), per block in LDS, then one atomic per
+// block, child and component. All loads are issued first.
+__global__ __launch_bounds__(kSelThreads) void k_ks_part(KdSoa E, int64_t n, SegTab T, SelTab S, int level,
+                                                         const int32_t* __restrict__ tile_seg) {
+  __shared__ SelRec cache[kSelCache];
+  __shared__ uint32_t lcnt[kSelCache * 2], lbase[kSelCache * 2];
+  __shared__ uint32_t lext[kSelCache * 2][6];
+  const SelTile st = sel_tile(T, S, level, true, tile_seg, cache);
+  const int k = level & 1, ko = k ^ 1;
+  const int lane = threadIdx.x & 63;
+  const int64_t t0 = (int64_t)blockIdx.x * kSelBlock;
+  if (!st.cached) {   // never at global levels; kept general
+    for (int it = 0; it < kSelIPT * kSelNSub; it++) {
+      const int64_t p = t0 + it * kSelThreads + threadIdx.x;
+      SelRec r;
+      const int j = p < n ? sel_find(T, S, level, true, st, cache, p, r) : -1;
+      if (j < 0) continue;
+      const float4 e = make_float4(E.comp(k, 0)[p], E.comp(k, 1)[p], E.comp(k, 2)[p], E.comp(k, 3)[p]);
+      const uint64_t key = (uint64_t)(orderable_key(coord_of(e, r.dim)) - r.kmin) << S.idbits |
+                           (uint32_t)__float_as_int(e.w);
+      if (key == r.med) continue;
+      const int side = key < r.med ? 0 : 1;
+      const int64_t dst = (int64_t)r.cb[side] + atomicAdd(&S.cnt[2 * j + side], 1u);
+      uint32_t* nx = S.ext[(level + 1) & 1] + (2 * (int64_t)j + side) * 6;
+      const uint32_t ok[3] = {orderable_key(e.x), orderable_key(e.y), orderable_key(e.z)};
+      for (int d = 0; d < 3; d++) {
+        atomicMin(&nx[d], ok[d]);
+        atomicMax(&nx[3 + d], ok[d]);
+      }
+      E.comp(ko, 0)[dst] = e.x;
+      E.comp(ko, 1)[dst] = e.y;
+      E.comp(ko, 2)[dst] = e.z;
+      E.comp(ko, 3)[dst] = e.w;
+    }
+    return;
+  }
+  const int nslot = st.jh - st.jl + 1;
+  for (int i = threadIdx.x; i < nslot * 2; i += kSelThreads) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      lext[i][d] = 0xFFFFFFFFu;
+      lext[i][3 + d] = 0u;
+    }
+  }
+  uint32_t amn[4][3], amx[4][3];   // groups 0..3 = slot 0 / 1 x side
+#pragma unroll
+  for (int g = 0; g < 4; g++)
+#pragma unroll
+    for (int d = 0; d < 3; d++) amn[g][d] = 0xFFFFFFFFu, amx[g][d] = 0u;
+  for (int sub = 0; sub < kSelNSub; sub++) {
+    const int64_t ts = t0 + (int64_t)sub * kSelTile;
+    for (int i = threadIdx.x; i < nslot * 2; i += kSelThreads) lcnt[i] = 0;
+    int sl[kSelIPT];
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {
+      const int64_t p = ts + it * kSelThreads + threadIdx.x;
+      sl[it] = p < n ? sel_slot(cache, nslot, p) : -1;
+    }
+    float4 e[kSelIPT];
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {   // every load issued before any is used
+      const int64_t p = sl[it] < 0 ? 0 : ts + it * kSelThreads + threadIdx.x;
+      e[it] = make_float4(E.comp(k, 0)[p], E.comp(k, 1)[p], E.comp(k, 2)[p], E.comp(k, 3)[p]);
+    }
+    __syncthreads();   // lcnt reset (and the previous sub-tile's lbase reads) done
+    int grp[kSelIPT];   // slot * 2 + side, -1: not moved
+    uint32_t rk[kSelIPT];
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {
+      int g = -1;
+      if (sl[it] >= 0) {
+        const SelRec& r = cache[sl[it]];
+        const uint64_t key = (uint64_t)(orderable_key(coord_of(e[it], r.dim)) - r.kmin) << S.idbits |
+                             (uint32_t)__float_as_int(e[it].w);
+        if (key != r.med) g = sl[it] * 2 + (key < r.med ? 0 : 1);   // the median is already a node
+      }
+      grp[it] = g;
+      rk[it] = 0;
+      uint64_t todo = __ballot(g >= 0);
+      while (todo) {
+        const int l = __ffsll((unsigned long long)todo) - 1;
+        const int gl = __shfl(g, l);
+        const uint64_t same = __ballot(g == gl) & todo;
+        uint32_t base = 0;
+        if (lane == l) base = atomicAdd(&lcnt[gl], (uint32_t)__popcll(same));
+        base = (uint32_t)__shfl((int)base, l);
+        if ((same >> lane) & 1) rk[it] = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+        todo &= ~same;
+      }
+      if (g >= 0) {
+        const uint32_t ok[3] = {orderable_key(e[it].x), orderable_key(e[it].y), orderable_key(e[it].z)};
+        if (g < 4) {
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int d = 0; d < 3; d++) {
+              amn[q][d] = g == q ? min(amn[q][d], ok[d]) : amn[q][d];
+              amx[q][d] = g == q ? max(amx[q][d], ok[d]) : amx[q][d];
+            }
+        } else {
+#pragma unroll
+          for (int d = 0; d < 3; d++) {
+            atomicMin(&lext[g][d], ok[d]);
+            atomicMax(&lext[g][3 + d], ok[d]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nslot * 2; i += kSelThreads) {
+      const uint32_t cn = lcnt[i];
+      lbase[i] = (uint32_t)cache[i >> 1].cb[i & 1] + (cn ? atomicAdd(&S.cnt[2 * (st.jl + (i >> 1)) + (i & 1)], cn) : 0u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kSelIPT; it++) {
+      if (grp[it] < 0) continue;
+      const int64_t dst = (int64_t)lbase[grp[it]] + rk[it];
+      E.comp(ko, 0)[dst] = e[it].x;
+      E.comp(ko, 1)[dst] = e[it].y;
+      E.comp(ko, 2)[dst] = e[it].z;
+      E.comp(ko, 3)[dst] = e[it].w;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const uint32_t mn = wave_minmax<false>(amn[q][d]), mx = wave_minmax<true>(amx[q][d]);
+      if (lane == 0 && q < nslot * 2 && mn <= mx) {
+        atomicMin(&lext[q][d], mn);
+        atomicMax(&lext[q][3 + d], mx);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nslot * 2; i += kSelThreads) {
+    if (lext[i][0] > lext[i][3]) continue;   // nothing went to this child from here
+    uint32_t* nx = S.ext[(level + 1) & 1] + (2 * (int64_t)(st.jl + (i >> 1)) + (i & 1)) * 6;
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      atomicMin(&nx[d], lext[i][d]);
+      atomicMax(&nx[3 + d], lext[i][3 + d]);
+    }
+  }
+}
+
+static hipError_t kd_build_sel(const float4* elems, int64_t n, float4* nodes, hipStream_t s) {
+  int H = 0;
+  while ((1ll << H) <= n) H++;          // levels = floor(log2 n) + 1
+  const int L0 = std::max(0, H - 10);   // subtrees at L0 hold <= 1023 elements
+  const int64_t cap = 1ll << (L0 + 1);  // subtree records down to level L0
+  int idbits = 1;
+  while ((1ll << idbits) < n) idbits++;
+  const int64_t nsc = 1ll << L0;        // subtrees at L0 (children of the last global level)
+  const bool global = L0 > 0;
+  DevBuf<float> soa((size_t)8 * n);
+  DevBuf<int32_t> tb(cap), ts(cap), tls(cap), tdim(cap), tid(cap), tsel(cap);
+  DevBuf<float> tco(cap), vlo(nsc), vsc(nsc);
+  DevBuf<uint32_t> ext((size_t)12 * nsc), kmin(nsc), rank(nsc), hist((size_t)256 * nsc), cnt(2 * nsc), ccnt(nsc);
+  DevBuf<int32_t> sdim(nsc), vbin(nsc), stb(nsc);
+  DevBuf<uint64_t> med(nsc), cand(global ? n : 0), cmin(nsc), cmax(nsc), cprefix(nsc);
+  DevBuf<int32_t> cshift(nsc);
+  DevBuf<uint32_t> cmatch(nsc), cnt2(nsc);
+  const bool bigsets = (1ll << H) > kCandCap;   // some subtree may exceed kCandCap candidates
+  DevBuf<uint64_t> cand2(global && bigsets ? n : 0);
+  const int64_t ntiles = (n + kSelBlock - 1) / kSelBlock;
+  DevBuf<int32_t> tile_seg(ntiles + 1);
+  if (!soa.p || !tb.p || !ts.p || !tls.p || !tdim.p || !tid.p || !tsel.p || !tco.p || !vlo.p || !vsc.p || !ext.p ||
+      !kmin.p || !rank.p || !hist.p || !cnt.p || !ccnt.p || !sdim.p || !vbin.p || !stb.p || !med.p ||
+      !tile_seg.p || !cmin.p || !cmax.p || !cprefix.p || !cshift.p || !cmatch.p || !cnt2.p ||
+      (global && !cand.p) || (global && bigsets && !cand2.p))
+    return hipErrorOutOfMemory;
+  const KdSoa E{soa.p, n};
+  SegTab T{tb.p, ts.p, tls.p, tdim.p, tco.p, tid.p, tsel.p};
+  SelTab S{{ext.p, ext.p + 6 * nsc}, sdim.p, kmin.p, vlo.p, vsc.p, vbin.p, rank.p, stb.p, med.p, hist.p, cnt.p,
+           ccnt.p, cand.p, cmin.p, cmax.p, cshift.p, cprefix.p, cmatch.p, cand2.p, cnt2.p, idbits};
+  const int32_t root[2] = {0, (int32_t)n};
+  PM_HIP_TRY(hipMemcpyAsync(tb.p, &root[0], 4, hipMemcpyHostToDevice, s));
+  PM_HIP_TRY(hipMemcpyAsync(ts.p, &root[1], 4, hipMemcpyHostToDevice, s));
+  const uint32_t ext0[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+  PM_HIP_TRY(hipMemcpyAsync(ext.p, ext0, sizeof(ext0), hipMemcpyHostToDevice, s));
+  if (global) PM_HIP_TRY(hipMemsetAsync(hist.p, 0, sizeof(uint32_t) * 256 * (size_t)(nsc / 2), s));
+  k_ks_init<<<(int)std::min<int64_t>(kInitBlocks, grid_for(n, 256)), 256, 0, s>>>(elems, n, E, ext.p);
+  PM_HIP_TRY(hipGetLastError());
+  for (int L = 0; L < L0; L++) {
+    const int64_t nseg = 1ll << L;
+    k_ks_seg<<<grid_for(nseg, 256), 256, 0, s>>>(L, cap, T, S);
+    PM_HIP_TRY(hipGetLastError());
+    k_kd_tileseg_n<<<grid_for(ntiles + 1, 256), 256, 0, s>>>(tb.p, L, ntiles, kSelBlock, tile_seg.p);
+    PM_HIP_TRY(hipGetLastError());
+    k_ks_hist<<<(int)ntiles, kSelThreads, 0, s>>>(E, n, T, S, L, tile_seg.p);
+    PM_HIP_TRY(hipGetLastError());
+    k_ks_find<<<(int)nseg, 64, 0, s>>>(S);
+    PM_HIP_TRY(hipGetLastError());
+    k_ks_compact<<<(int)ntiles, kSelThreads, 0, s>>>(E, n, T, S, L, tile_seg.p);
+    PM_HIP_TRY(hipGetLastError());
+    k_ks_cinit<<<grid_for(nseg, 256), 256, 0, s>>>(nseg, S);
+    PM_HIP_TRY(hipGetLastError());
+    const bool big = (1ll << (H - L)) > kCandCap;   // a subtree may hold more than kCandCap candidates
+    if (big) {
+      const dim3 g(std::max(1, 1024 >> L), (unsigned)nseg);
+      for (int pass = 0; pass < 8; pass++) {   // <= 61 key bits: every set reaches one key
+        k_ks_chist<<<g, kSelThreads, 0, s>>>(L, T, S);
+        PM_HIP_TRY(hipGetLastError());
+        k_ks_cfind<<<(int)nseg, 64, 0, s>>>(S);
+        PM_HIP_TRY(hipGetLastError());
+      }
+      k_ks_cgather<<<g, kSelThreads, 0, s>>>(L, T, S);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    k_ks_cand<<<(int)nseg, kCandThreads, 0, s>>>(L, T, S, elems, nodes, big);
+    PM_HIP_TRY(hipGetLastError());
+    k_ks_part<<<(int)ntiles, kSelThreads, 0, s>>>(E, n, T, S, L, tile_seg.p);
+    PM_HIP_TRY(hipGetLastError());
+  }
+  k_kd_local<true><<<(int)nsc, kLocal, 0, s>>>(KdLists{}, E, L0, T, nodes);
+  return hipGetLastError();
+}
+
+#ifndef PM_KD_SEL
+#define PM_KD_SEL 1   // the selection build (production); 0: the presorted build only
+#endif
+// Below this size the presorted build is faster (the selection build's ~10
+// launches per level dominate): 45.4 M elements 21.4 vs 24.5 ms, 10 M 6.0 vs
+// 5.7 ms, 1 M 2.0 vs 1.0 ms (tools/kd_probe.py). Same tree either way.
+#ifndef PM_KD_SEL_MIN
+#define PM_KD_SEL_MIN (1 << 24)
+#endif
+
+static hipError_t kd_build_lists(const float4* elems, int64_t n, float4* nodes, hipStream_t s);
+
 hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n >= kMaxMapPhotons) return hipErrorInvalidValue;
+  // the check variant keeps the presorted build (the identical-tree tests
+  // compare the two libraries)
+  if (PM_KD_SEL && !PM_CHECK_VARIANT && n >= PM_KD_SEL_MIN) return kd_build_sel(elems, n, nodes, s);
+  return kd_build_lists(elems, n, nodes, s);
+}
+
+// The presorted build (rounds 1-2; the check variant's).
+static hipError_t kd_build_lists(const float4* elems, int64_t n, float4* nodes, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (n >= kMaxMapPhotons) return hipErrorInvalidValue;
   int H = 0;
@@ -783,7 +1799,7 @@ hipError_t kd_build(const float4* elems, int64_t n, float4* nodes, hipStream_t s
   const int L0 = PM_CHECK_VARIANT ? H : std::max(0, H - 10);
   for (int L = 0; L < H; L++) {
     if (L == L0) {
-      k_kd_local<<<(int)(1ll << L0), kLocal, 0, s>>>(Lst, L0, T, nodes);
+      k_kd_local<false><<<(int)(1ll << L0), kLocal, 0, s>>>(Lst, KdSoa{}, L0, T, nodes);
       PM_HIP_TRY(hipGetLastError());
       break;
     }

@@ -59,6 +59,11 @@ class FrameConfig:
     # the caustic map (pm_render_gather_caustic), i.e. beside the global map's
     # kd build, instead of beside the global gather in finish
     early_caustic_gather: bool = False
+    # one rank: the render side thread traces the caustic photons and builds
+    # their map beside the global trace, then holds pm_render_begin until the
+    # global trace is done, so the render's latency-bound ray kernels run beside
+    # the bandwidth-bound kd build instead of beside the trace
+    begin_after_trace: bool = False
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -383,7 +388,7 @@ class GpuBackend:
         pm, c = self.pm, self.cfg
         if getattr(self, "_rside", None) is None:
             self._rside = torch.cuda.Stream()
-        side, box = self._rside, {"c_ready": threading.Event()}
+        side, box = self._rside, {"c_ready": threading.Event(), "trace_done": threading.Event()}
         device = side.device   # this rank's GPU (the caller's current device)
 
         def run():
@@ -393,10 +398,16 @@ class GpuBackend:
                 # would allocate its tensors (torch.empty(device="cuda")) on GPU 0
                 # (the library itself follows the stream's device, include/pm.h)
                 torch.cuda.set_device(device)
-                job = pm.render_begin(self.scene, self.cam, c.width, c.height, c.spp, c.depth, c.sky, self.lights,
-                                      tile_rank=tile_rank, tile_count=tile_count, stream=side.cuda_stream,
-                                      caustic_k=c.caustic_k)
-                box["r"] = (job, pm.phase_us("paths"))   # phase timers are per host thread
+                def begin():
+                    j = pm.render_begin(self.scene, self.cam, c.width, c.height, c.spp, c.depth, c.sky, self.lights,
+                                        tile_rank=tile_rank, tile_count=tile_count, stream=side.cuda_stream,
+                                        caustic_k=c.caustic_k)
+                    box["r"] = (j, pm.phase_us("paths"))   # phase timers are per host thread
+                    return j
+
+                late = c.begin_after_trace and caustic_shard is not None and caustic_map
+                if not late:
+                    job = begin()
                 if caustic_shard is not None:
                     t = pm.run_point_light_ray_gen(self.scene, self.lights, c.caustic, c.max_depth, True,
                                                    shard_rank=caustic_shard[0], shard_count=caustic_shard[1],
@@ -406,6 +417,9 @@ class GpuBackend:
                     if caustic_map:
                         cm = pm.PhotonMap(t, pm.CAUSTICS_PHOTON_POWER, stream=side.cuda_stream)
                         box["cm"] = (cm, pm.phase_us("kdbuild"))
+                        if late:
+                            box["trace_done"].wait()
+                            job = begin()
                         if c.early_caustic_gather:
                             job.gather_caustic(cm, stream=side.cuda_stream)
             except BaseException as e:   # re-raised by finish_render / join_render
@@ -438,8 +452,14 @@ class GpuBackend:
         return cm
 
     @staticmethod
+    def trace_done(pending):
+        """The global trace is over (begin_after_trace's thread may go on)."""
+        pending[1]["trace_done"].set()
+
+    @staticmethod
     def join_render(pending):
         th, box = pending
+        box["trace_done"].set()   # never leave the thread waiting
         th.join()
         if "e" in box:
             raise box["e"]
@@ -509,6 +529,8 @@ def _maps(backend, rank: int, world: int, dist, pending=None, early_caustic: boo
     come from its thread; with early_caustic (world 1), so does the caustic map
     (returned as None here)."""
     g = backend.trace(False, rank, world)
+    if pending is not None and hasattr(backend, "trace_done"):
+        backend.trace_done(pending)
     c = backend.caustic_photons(pending) if pending is not None else backend.trace(True, rank, world)
     if backend.cfg.quantize:   # elementwise: the same before or after the exchange
         g, c = backend.quantize(g), backend.quantize(c)

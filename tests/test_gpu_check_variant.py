@@ -47,7 +47,7 @@ def runs(tmp_path_factory):
 KEYS = ["cloud_hits", "cloud_occ", "cloud_photons", "cornell_g", "cornell_c", "cornell_gmap", "cornell_cmap",
         "gather_g", "gather_c", "gather_e", "gather_k200", "gather_k256", "knn_ids", "knn_d2", "knn_md", "render_64_rgba", "render_64_rgb",
         "render_64_stats", "render_40_rgba", "render_40_rgb", "render_40_stats", "kd_5", "kd_1023", "kd_1024",
-        "kd_70000", "kd_2000003", "sphere_g", "sphere_c", "sphere_rgb", "sphere_stats"]
+        "kd_70000", "kd_2000003", "kd_same_5000", "kd_wall_300001", "kd_special_70001", "sphere_g", "sphere_c", "sphere_rgb", "sphere_stats"]
 FULL = ["c3_counts", "c3_g_crc", "c3_c_crc", "c3_gmap_crc", "c3_stats", "c3_rgba", "c3_rgb",
         "c5_counts", "c5_c_crc", "c5_cmap_crc", "c5_stats", "c5_rgba", "c5_rgb"]
 

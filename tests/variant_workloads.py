@@ -43,12 +43,25 @@ CLOUD_MAT = np.array([0.7, 0.6, 0.5, 0.6, 0.2, 0.2, 1.5], np.float32)
 CLOUD_LIGHTS = [dict(pos=(0.1, 0.2, 0.3), rgb=(1, 1, 1), power=100.0)]
 
 
-def kd_records(n, seed):
+def kd_records(n, seed, kind="ties"):
     rng = np.random.default_rng(seed)
     rec = np.zeros((n, 11), np.float32)
     rec[:, 0:3] = rng.uniform(-20, 20, size=(n, 3))
-    rec[: n // 7, 2] = 1.5          # ties on one axis
-    rec[n // 7: n // 5, 0:3] = 5.0  # exact duplicates
+    if kind == "ties":
+        rec[: n // 7, 2] = 1.5          # ties on one axis
+        rec[n // 7: n // 5, 0:3] = 5.0  # exact duplicates
+    elif kind == "same":                # one repeated point
+        rec[:, 0:3] = (1.0, -2.0, 3.0)
+    elif kind == "wall":                # most points on axis planes (Cornell-like)
+        f = rng.integers(0, 4, size=n)
+        rec[f == 0, 0] = -10.0
+        rec[f == 1, 1] = 0.0
+        rec[f == 2, 2] = 10.0
+    elif kind == "special":             # signed zeros and infinities
+        rec[::5, 0] = -0.0
+        rec[1::5, 1] = 0.0
+        rec[2::11, 2] = np.inf
+        rec[3::13, 0] = -np.inf
     rec[:, 6:9] = rng.uniform(0, 1, size=(n, 3))
     rec[:, 9] = 1.0
     return rec
@@ -105,6 +118,10 @@ def run(full: bool = False) -> dict:
         t = torch.from_numpy(kd_records(n, 100 + n)).cuda()
         pm_amd.build_tree(t)
         out[f"kd_{n}"] = t.cpu().numpy()
+    for kind, n in (("same", 5000), ("wall", 300001), ("special", 70001)):
+        t = torch.from_numpy(kd_records(n, 7 + n, kind)).cuda()
+        pm_amd.build_tree(t)
+        out[f"kd_{kind}_{n}"] = t.cpu().numpy()
     # 4. sphere scene (glass): photons and a render
     meshes, lights = pm_amd.load_scene_file(os.path.join(HERE, "golden", "scenes", "sphere", "sphere.glb"))
     ss = pm_amd.Scene(meshes)

@@ -1,37 +1,25 @@
-"""Per-kernel totals from a rocprofv3 SQLite output (run_results.db):
-python tools/rocpd_stats.py DB [--frames N] [--top K] [--csv OUT]."""
-import argparse
-import csv
+"""Per-kernel stats (ms per frame) from a rocprofv3 rocpd SQLite database:
+    python3 tools/rocpd_stats.py DB FRAMES [MIN_GRID_THREADS]
+MIN_GRID_THREADS keeps only dispatches with at least that many threads (to
+separate a large build's launches from small ones)."""
 import sqlite3
-
-
-def kernel_stats(db):
-    con = sqlite3.connect(db)
-    cols = [r[1] for r in con.execute("pragma table_info(kernels)")]
-    name = "name" if "name" in cols else "kernel_name"
-    rows = con.execute(f"select {name}, count(*), sum(end - start), avg(end - start) from kernels "
-                       f"group by {name} order by sum(end - start) desc").fetchall()
-    return [(n, c, tot, avg) for n, c, tot, avg in rows]
+import sys
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("db")
-    ap.add_argument("--frames", type=float, default=1.0)
-    ap.add_argument("--top", type=int, default=30)
-    ap.add_argument("--csv")
-    a = ap.parse_args()
-    rows = kernel_stats(a.db)
-    total = sum(r[2] for r in rows)
-    for n, c, tot, avg in rows[: a.top]:
-        print(f"{n.split('(')[0][:58]:58s} calls={c:5d} ms/frame={tot / 1e6 / a.frames:8.2f} "
-              f"avg_us={avg / 1e3:9.1f} {100 * tot / total:5.1f}%")
-    if a.csv:
-        with open(a.csv, "w", newline="") as f:
-            w = csv.writer(f)
-            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
-            for n, c, tot, avg in rows:
-                w.writerow([n, c, tot, avg, 100 * tot / total])
+    db = sys.argv[1]
+    frames = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
+    min_grid = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    c = sqlite3.connect(db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    name = "kernel_name" if "kernel_name" in cols else "name"
+    where = f"where grid_x * grid_y * grid_z >= {min_grid}" if min_grid and "grid_x" in cols else ""
+    rows = c.execute(f"select {name}, count(*), sum(end - start), avg(end - start) from kernels {where} "
+                     f"group by {name} order by sum(end - start) desc").fetchall()
+    tot = sum(r[2] for r in rows)
+    for n, cnt, s, a in rows:
+        print(f"{n.split('(')[0][:64]:64s} calls={cnt:5d} ms/frame={s / 1e6 / frames:8.3f} avg_us={a / 1e3:9.1f}")
+    print(f"total kernel ms/frame {tot / 1e6 / frames:.2f}")
 
 
 if __name__ == "__main__":
