@@ -590,6 +590,16 @@ __device__ __forceinline__ uint32_t wave_minmax(uint32_t v) {
   return op(op(a, b), op(c, d));
 }
 
+// u64 min / max over a wave: the high words first, then the low words of the
+// lanes that hold the extreme high word
+template <bool MAX>
+__device__ __forceinline__ uint64_t wave_minmax64(uint64_t v) {
+  const uint32_t hi = (uint32_t)(v >> 32);
+  const uint32_t h = wave_minmax<MAX>(hi);
+  const uint32_t lo = hi == h ? (uint32_t)v : (MAX ? 0u : 0xFFFFFFFFu);
+  return (uint64_t)h << 32 | wave_minmax<MAX>(lo);
+}
+
 // Block-wide bitonic sort (blockDim = kLocal, one (key, slot) pair per thread,
 // ascending over the first n2 threads, n2 a power of two >= 64): strides below
 // 64 exchange through wave shuffles, larger ones through LDS (kx / vx).
@@ -1266,6 +1276,7 @@ __global__ __launch_bounds__(kSelThreads) void k_ks_compact(KdSoa E, int64_t n, 
     lkmin[threadIdx.x] = ~0ull;
     lkmax[threadIdx.x] = 0ull;
   }
+  uint64_t kmn0 = ~0ull, kmx0 = 0ull, kmn1 = ~0ull, kmx1 = 0ull;   // key range of slots 0 / 1 (this lane)
   for (int sub = 0; sub < kSelNSub; sub++) {
     const int64_t ts = t0 + (int64_t)sub * kSelTile;
     if (threadIdx.x < nslot) lcc[threadIdx.x] = 0;
@@ -1298,26 +1309,21 @@ __global__ __launch_bounds__(kSelThreads) void k_ks_compact(KdSoa E, int64_t n, 
       const int g = sl[it];
       key[it] = g >= 0 ? (uint64_t)(orderable_key(cv[it]) - cache[g].kmin) << S.idbits | idv[it] : 0ull;
       rk[it] = 0;
+      if (g == 0) kmn0 = min(kmn0, key[it]), kmx0 = max(kmx0, key[it]);
+      else if (g == 1) kmn1 = min(kmn1, key[it]), kmx1 = max(kmx1, key[it]);
+      else if (g > 1) {
+        atomicMin(&lkmin[g], (unsigned long long)key[it]);
+        atomicMax(&lkmax[g], (unsigned long long)key[it]);
+      }
       uint64_t todo = __ballot(g >= 0);
       while (todo) {
         const int l = __ffsll((unsigned long long)todo) - 1;
         const int gl = __shfl(g, l);
         const uint64_t same = __ballot(g == gl) & todo;
-        const bool in = (same >> lane) & 1;
-        unsigned long long mn = in ? key[it] : ~0ull, mx = in ? key[it] : 0ull;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          mn = min(mn, (unsigned long long)__shfl_xor(mn, o));
-          mx = max(mx, (unsigned long long)__shfl_xor(mx, o));
-        }
         uint32_t base = 0;
-        if (lane == l) {
-          base = atomicAdd(&lcc[gl], (uint32_t)__popcll(same));
-          atomicMin(&lkmin[gl], mn);
-          atomicMax(&lkmax[gl], mx);
-        }
+        if (lane == l) base = atomicAdd(&lcc[gl], (uint32_t)__popcll(same));
         base = (uint32_t)__shfl((int)base, l);
-        if (in) rk[it] = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+        if ((same >> lane) & 1) rk[it] = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
         todo &= ~same;
       }
     }
@@ -1331,6 +1337,15 @@ __global__ __launch_bounds__(kSelThreads) void k_ks_compact(KdSoa E, int64_t n, 
     for (int it = 0; it < kSelIPT; it++)
       if (sl[it] >= 0) S.cand[(int64_t)cache[sl[it]].b + lbase[sl[it]] + rk[it]] = key[it];
   }
+  {
+    const uint64_t a0 = wave_minmax64<false>(kmn0), b0 = wave_minmax64<true>(kmx0);
+    const uint64_t a1 = wave_minmax64<false>(kmn1), b1 = wave_minmax64<true>(kmx1);
+    if (lane == 0) {
+      if (a0 <= b0) atomicMin(&lkmin[0], (unsigned long long)a0), atomicMax(&lkmax[0], (unsigned long long)b0);
+      if (a1 <= b1) atomicMin(&lkmin[1], (unsigned long long)a1), atomicMax(&lkmax[1], (unsigned long long)b1);
+    }
+  }
+  __syncthreads();
   if (threadIdx.x < nslot && lkmin[threadIdx.x] <= lkmax[threadIdx.x]) {
     const int j = st.jl + threadIdx.x;
     atomicMin((unsigned long long*)&S.cmin[j], lkmin[threadIdx.x]);
@@ -1518,7 +1533,11 @@ __global__ __launch_bounds__(kCandThreads) void k_ks_cand(int level, SegTab T, S
 // every element to its child range; the children's extents reduced per lane
 // (the block's first two subtrees), per block in LDS, then one atomic per
 // block, child and component. All loads are issued first.
-__global__ __launch_bounds__(kSelThreads) void k_ks_part(KdSoa E, int64_t n, SegTab T, SelTab S, int level,
+#ifndef PM_KS_PART_WAVES
+#define PM_KS_PART_WAVES 0   // occupancy target of k_ks_part (0: compiler's choice)
+#endif
+__global__ __launch_bounds__(kSelThreads) PM_WAVES_ATTR(PM_KS_PART_WAVES) void k_ks_part(KdSoa E, int64_t n, SegTab T,
+                                                                                      SelTab S, int level,
                                                          const int32_t* __restrict__ tile_seg) {
   __shared__ SelRec cache[kSelCache];
   __shared__ uint32_t lcnt[kSelCache * 2], lbase[kSelCache * 2];
