@@ -1445,36 +1445,31 @@ __global__ __launch_bounds__(kSelThreads) void k_ks_cgather(int level, SegTab T,
   }
 }
 
-// one workgroup per subtree: the candidate of the median's rank. While more
-// than kCandThreads keys match the selected prefix, an 8-bit radix pass over
-// them (LDS histogram); then the matching keys are sorted in LDS. Writes the
-// median's key and its node (position from elems[index]).
-__global__ __launch_bounds__(kCandThreads) void k_ks_cand(int level, SegTab T, SelTab S,
-                                                          const float4* __restrict__ elems,
-                                                          float4* __restrict__ nodes, bool gathered) {
-  __shared__ uint32_t h[256];
-  __shared__ uint64_t lk[kCandThreads], kx[kCandThreads];
-  __shared__ int16_t vx[kCandThreads];
-  __shared__ uint64_t s_prefix;
-  __shared__ uint32_t s_rank, s_cnt;
-  __shared__ int s_shift;
-  const int j = blockIdx.x, tid = threadIdx.x;
-  if (S.dim[j] < 0) return;
-  const int64_t t = (1ll << level) - 1 + j;
-  const bool big = gathered && S.ccnt[j] > (uint32_t)kCandCap;   // k_ks_cgather ran for it
-  const uint64_t* cand = (big ? S.cand2 : S.cand) + T.b[t];
-  const uint32_t total = big ? S.cnt2[j] : S.ccnt[j];
-  uint32_t rank = S.rank[j], c = S.cmatch[j];
-  uint64_t prefix = S.cprefix[j];
-  int shift = S.cshift[j];
+// The candidate of rank `rank` among the `total` keys at cand (global) whose
+// bits above `shift` equal `prefix` (c of them): while more than kCandThreads
+// match, an 8-bit radix pass over them (LDS histogram); then the matching keys
+// are sorted in LDS. Writes the median's key and its node (position from
+// elems[index]). Called by a whole kCandThreads-thread workgroup.
+struct CandShared {
+  uint32_t h[256];
+  uint64_t lk[kCandThreads], kx[kCandThreads];
+  int16_t vx[kCandThreads];
+  uint64_t prefix;
+  uint32_t rank, cnt;
+  int shift;
+};
+__device__ __forceinline__ void cand_pick(CandShared& sh, const uint64_t* cand, uint32_t total, uint32_t rank,
+                                          uint32_t c, uint64_t prefix, int shift, int j, int64_t t, SegTab T,
+                                          SelTab S, const float4* __restrict__ elems, float4* __restrict__ nodes) {
+  const int tid = threadIdx.x;
   while (c > kCandThreads && shift > 0) {   // keys are unique: c == 1 once shift == 0
     const int w = min(8, shift);
-    h[tid] = 0;
+    sh.h[tid] = 0;
     if (tid == 0) {   // a rank outside the histogram ends the loop (never, with consistent counts)
-      s_prefix = prefix;
-      s_rank = rank;
-      s_cnt = 0;
-      s_shift = 0;
+      sh.prefix = prefix;
+      sh.rank = rank;
+      sh.cnt = 0;
+      sh.shift = 0;
     }
     __syncthreads();
     for (uint32_t i0 = 0; i0 < total; i0 += kCandThreads) {
@@ -1484,43 +1479,43 @@ __global__ __launch_bounds__(kCandThreads) void k_ks_cand(int level, SegTab T, S
         const uint64_t key = cand[i];
         if ((key >> shift) == prefix) bin = (int)((key >> (shift - w)) & ((1u << w) - 1u));
       }
-      merged_add(h, bin, 2);
+      merged_add(sh.h, bin, 2);
     }
     __syncthreads();
     if (tid < 64) {
-      const uint4 c4 = reinterpret_cast<const uint4*>(h)[tid];
+      const uint4 c4 = reinterpret_cast<const uint4*>(sh.h)[tid];
       uint32_t r, cb;
       int bin;
       if (wave_pick_bin(c4, rank, bin, r, cb)) {
-        s_prefix = prefix << w | (uint64_t)bin;
-        s_rank = r;
-        s_cnt = cb;
-        s_shift = shift - w;
+        sh.prefix = prefix << w | (uint64_t)bin;
+        sh.rank = r;
+        sh.cnt = cb;
+        sh.shift = shift - w;
       }
     }
     __syncthreads();
-    prefix = s_prefix;
-    rank = s_rank;
-    c = s_cnt;
-    shift = s_shift;
+    prefix = sh.prefix;
+    rank = sh.rank;
+    c = sh.cnt;
+    shift = sh.shift;
     __syncthreads();
   }
-  if (tid == 0) s_cnt = 0;
+  if (tid == 0) sh.cnt = 0;
   __syncthreads();
   for (uint32_t i = tid; i < total; i += kCandThreads) {
     const uint64_t key = cand[i];
     if ((key >> shift) == prefix) {
-      const uint32_t o = atomicAdd(&s_cnt, 1u);
-      if (o < kCandThreads) lk[o] = key;
+      const uint32_t o = atomicAdd(&sh.cnt, 1u);
+      if (o < kCandThreads) sh.lk[o] = key;
     }
   }
   __syncthreads();
-  c = min(s_cnt, (uint32_t)kCandThreads);
+  c = min(sh.cnt, (uint32_t)kCandThreads);
   int n2 = 64;
   while (n2 < (int)c) n2 <<= 1;
-  uint64_t key = tid < (int)c ? lk[tid] : ~0ull;
+  uint64_t key = tid < (int)c ? sh.lk[tid] : ~0ull;
   int v = tid;
-  block_bitonic(key, v, n2, kx, vx);
+  block_bitonic(key, v, n2, sh.kx, sh.vx);
   if (tid == (int)rank) {
     S.med[j] = key;
     const int id = (int)(key & ((1ull << S.idbits) - 1ull));
@@ -1530,6 +1525,125 @@ __global__ __launch_bounds__(kCandThreads) void k_ks_cand(int level, SegTab T, S
     T.coord[t] = coord_of(e, dim);
     nodes[t] = make_float4(e.x, e.y, e.z, __int_as_float((id << 2) | dim));
   }
+}
+
+// one workgroup per subtree: the candidate of the median's rank (after the
+// grid-wide passes for large sets)
+__global__ __launch_bounds__(kCandThreads) void k_ks_cand(int level, SegTab T, SelTab S,
+                                                          const float4* __restrict__ elems,
+                                                          float4* __restrict__ nodes, bool gathered) {
+  __shared__ CandShared sh;
+  const int j = blockIdx.x;
+  if (S.dim[j] < 0) return;
+  const int64_t t = (1ll << level) - 1 + j;
+  const bool big = gathered && S.ccnt[j] > (uint32_t)kCandCap;   // k_ks_cgather ran for it
+  const uint64_t* cand = (big ? S.cand2 : S.cand) + T.b[t];
+  const uint32_t total = big ? S.cnt2[j] : S.ccnt[j];
+  cand_pick(sh, cand, total, S.rank[j], S.cmatch[j], S.cprefix[j], S.cshift[j], j, t, T, S, elems, nodes);
+}
+
+// Deep levels (subtrees of <= kSegSelMax elements, enough of them to fill the
+// GPU): one workgroup per subtree does the whole selection over its own
+// contiguous range -- histogram, bin pick, compaction of the bin's keys into
+// its candidate range (with their key range), cand_pick -- in one launch
+// instead of five, reading the split coordinate twice (the second time from L2).
+constexpr int kSegSelMax = 1 << 17;
+#ifndef PM_KS_SEGSEL_MIN
+#define PM_KS_SEGSEL_MIN 512   // subtrees per level for k_ks_segsel (fewer workgroups underfill the GPU)
+#endif
+constexpr int64_t kSegSelMinSegs = PM_KS_SEGSEL_MIN;
+#ifndef PM_KS_SEGSEL_U
+#define PM_KS_SEGSEL_U 8
+#endif
+__global__ __launch_bounds__(kCandThreads) void k_ks_segsel(KdSoa E, int level, SegTab T, SelTab S,
+                                                            const float4* __restrict__ elems,
+                                                            float4* __restrict__ nodes) {
+  __shared__ CandShared sh;
+  __shared__ int s_bin;
+  __shared__ uint32_t s_rank, s_cb, s_n;
+  __shared__ unsigned long long s_kmin, s_kmax;
+  const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  if (S.dim[j] < 0) return;
+  const int64_t t = (1ll << level) - 1 + j;
+  const int b = T.b[t], s = T.s[t], dim = S.dim[j];
+  const uint32_t kmin = S.kmin[j];
+  const float lo = S.vlo[j], sc = S.vsc[j];
+  const int k = level & 1;
+  const float* cd = E.comp(k, dim) + b;
+  const float* ci = E.comp(k, 3) + b;
+  sh.h[tid] = 0;
+  if (tid == 0) {
+    s_bin = -1;
+    s_n = 0;
+    s_kmin = ~0ull;
+    s_kmax = 0ull;
+  }
+  __syncthreads();
+  constexpr int U = PM_KS_SEGSEL_U;   // loads in flight per thread
+  for (int i0 = 0; i0 < s; i0 += U * kCandThreads) {
+    float cv[U];
+#pragma unroll
+    for (int q = 0; q < U; q++) {
+      const int i = i0 + q * kCandThreads + tid;
+      cv[q] = i < s ? cd[i] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < U; q++) {
+      const int i = i0 + q * kCandThreads + tid;
+      merged_add(sh.h, i < s ? vbin_of(cv[q], lo, sc) : -1, 2);
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const uint4 c4 = reinterpret_cast<const uint4*>(sh.h)[tid];
+    uint32_t r, cb;
+    int bin;
+    if (wave_pick_bin(c4, S.rank[j], bin, r, cb)) {
+      s_bin = bin;
+      s_rank = r;
+      s_cb = cb;
+    }
+  }
+  __syncthreads();
+  const int bin = s_bin;
+  if (bin < 0) return;   // inconsistent counts (never): leave the node unwritten
+  uint64_t* cand = S.cand + b;
+  uint64_t kmn = ~0ull, kmx = 0ull;
+  for (int i0 = 0; i0 < s; i0 += U * kCandThreads) {
+    float cv[U];
+#pragma unroll
+    for (int q = 0; q < U; q++) {
+      const int i = i0 + q * kCandThreads + tid;
+      cv[q] = i < s ? cd[i] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < U; q++) {
+      const int i = i0 + q * kCandThreads + tid;
+      const bool take = i < s && vbin_of(cv[q], lo, sc) == bin;
+      const uint64_t m = __ballot(take);
+      if (!m) continue;
+      const int l = __ffsll((unsigned long long)m) - 1;
+      uint32_t base = 0;
+      if (lane == l) base = atomicAdd(&s_n, (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, l);
+      if (take) {
+        const uint64_t key = (uint64_t)(orderable_key(cv[q]) - kmin) << S.idbits | (uint32_t)__float_as_int(ci[i]);
+        cand[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = key;
+        kmn = min(kmn, key);
+        kmx = max(kmx, key);
+      }
+    }
+  }
+  kmn = wave_minmax64<false>(kmn);
+  kmx = wave_minmax64<true>(kmx);
+  if (lane == 0 && kmn <= kmx) {
+    atomicMin(&s_kmin, (unsigned long long)kmn);
+    atomicMax(&s_kmax, (unsigned long long)kmx);
+  }
+  __syncthreads();   // the candidates (global, this workgroup's) and their range are complete
+  const uint64_t a = s_kmin, z = s_kmax;
+  const int shift = (a ^ z) ? 64 - __clzll((long long)(a ^ z)) : 0;
+  cand_pick(sh, cand, s_cb, s_rank, s_cb, shift >= 64 ? 0ull : a >> shift, shift, j, t, T, S, elems, nodes);
 }
 
 // every element to its child range; the children's extents reduced per lane
@@ -1728,6 +1842,13 @@ static hipError_t kd_build_sel(const float4* elems, int64_t n, float4* nodes, hi
     PM_HIP_TRY(hipGetLastError());
     k_kd_tileseg_n<<<grid_for(ntiles + 1, 256), 256, 0, s>>>(tb.p, L, ntiles, kSelBlock, tile_seg.p);
     PM_HIP_TRY(hipGetLastError());
+    if ((1ll << (H - L)) <= kSegSelMax && nseg >= kSegSelMinSegs) {   // deep level: one workgroup per subtree
+      k_ks_segsel<<<(int)nseg, kCandThreads, 0, s>>>(E, L, T, S, elems, nodes);
+      PM_HIP_TRY(hipGetLastError());
+      k_ks_part<<<(int)ntiles, kSelThreads, 0, s>>>(E, n, T, S, L, tile_seg.p);
+      PM_HIP_TRY(hipGetLastError());
+      continue;
+    }
     k_ks_hist<<<(int)ntiles, kSelThreads, 0, s>>>(E, n, T, S, L, tile_seg.p);
     PM_HIP_TRY(hipGetLastError());
     k_ks_find<<<(int)nseg, 64, 0, s>>>(S);
