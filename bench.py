@@ -102,6 +102,30 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
     }
 
 
+def secondary_config2(args):
+    """The Cornell-box line (config 2, north_star's second workload) measured in a
+    child process (its own device buffers and scene; this process's stay
+    allocated), so the default bench line carries both configurations. The
+    child is a plain `bench.py --config 2` run: same clock, same contract."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--config", "2", "--steps", str(max(10, args.steps)),
+           "--warmup", str(max(3, args.warmup)), "--no-cpu-baseline", "--no-secondary"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+        if r.returncode != 0 or not line:
+            return {"error": f"exit {r.returncode}: {r.stderr.strip()[-400:]}"}
+        d = json.loads(line[-1])
+    except Exception as e:   # reported, never fatal to the main line
+        return {"error": repr(e)}
+    keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_frame", "config", "phases_ms", "photon_maps",
+            "render")
+    res = {k: d[k] for k in keep if k in d}
+    res["roofline_frac"] = d.get("roofline", {}).get("frac")
+    res["command"] = " ".join(["python", "bench.py"] + cmd[2:])
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -125,6 +149,9 @@ def main():
     ap.add_argument("--frame-opt", action="append", default=[], metavar="FIELD=0|1",
                     help="override a boolean pm_amd.dist.FrameConfig field (A/B runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="config 3 at N=1 also measures config 2 (the reference's Cornell box) in a child "
+                         "process and reports it under 'secondary'; this turns that off")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: every CPU this process may use, see host_cores)")
     ap.add_argument("--cpu-sample-photons", type=int, default=2_000_000)
@@ -283,6 +310,8 @@ def main():
                      "avg_launch_ms": round(t_g * 1e3, 3)},
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and args.config == 3 and not args.no_secondary:
+        out["secondary"] = {"config2": secondary_config2(args)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(meshes, lights, args, info["n_global"],
                                            args.cpu_threads or host_cores()[0])

@@ -4,7 +4,7 @@ set -u
 mkdir -p gpurun_out/gexp
 export TMPDIR=/tmp
 for d in ${DIAG:-13}; do
-  (cd /tmp && PM_GATHER_MODE=$d timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/gexp/p$d -o m$d -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/gexp/p$d.log 2>&1) || exit 3
+  (cd /tmp && PM_GATHER_MODE=$d timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/gexp/p$d -o m$d -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary > $GRAFT_REPO_ROOT/gpurun_out/gexp/p$d.log 2>&1) || exit 3
   python3 - "$d" <<'PY'
 import csv, glob, sys
 f = glob.glob(f"gpurun_out/gexp/p{sys.argv[1]}/**/*kernel_stats.csv", recursive=True)[0]

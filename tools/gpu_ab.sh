@@ -9,7 +9,7 @@ for v in "$@"; do
   L=$R/photon-mapping_amd/$v/libpm_hip.so
   [ -f $L ] || { echo "no $v"; continue; }
   tag=$(echo "$v $ARGS" | tr -c 'a-zA-Z0-9_\n' '_')
-  PM_HIP_LIB=$L timeout -k 10 300 python -u bench.py $ARGS --no-cpu-baseline > gpurun_out/ab/$tag.log 2>&1 || { echo AB_FAILED $v; tail -20 gpurun_out/ab/$tag.log; exit 1; }
+  PM_HIP_LIB=$L timeout -k 10 300 python -u bench.py $ARGS --no-cpu-baseline --no-secondary > gpurun_out/ab/$tag.log 2>&1 || { echo AB_FAILED $v; tail -20 gpurun_out/ab/$tag.log; exit 1; }
   python3 -c "
 import json,sys
 d=json.loads(open('gpurun_out/ab/$tag.log').read().strip().splitlines()[-1])

@@ -9,7 +9,7 @@ tail -1 gpurun_out/ab/tests.log
 for rep in $(seq ${REPS:-2}); do
   for v in default $VARIANTS; do
     if [ $v = default ]; then unset PM_HIP_LIB; else export PM_HIP_LIB=photon-mapping_amd/$v/libpm_hip.so; fi
-    timeout -k 10 200 python bench.py --no-cpu-baseline --steps 3 > gpurun_out/ab/b.log 2>&1 || { tail gpurun_out/ab/b.log; exit 2; }
+    timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary --steps 3 > gpurun_out/ab/b.log 2>&1 || { tail gpurun_out/ab/b.log; exit 2; }
     python - "$v" <<'PY'
 import json, sys
 line = [l for l in open("gpurun_out/ab/b.log") if l.startswith("{")][-1]
