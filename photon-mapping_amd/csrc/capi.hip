@@ -519,6 +519,7 @@ int pm_photon_map_destroy(pm_photon_map* m) {
 struct pm_kd_shard_plan {
   DevBuf<float4> elems, payload, top;
   DevBuf<uint8_t> sub;   // subtree of every element (255: a top node)
+  DevBuf<uint32_t> boff;  // per-tile subtree starts (kd_shard_offsets), made by the first build
   int64_t n = 0;
   int L = 0;   // 0: not split
   std::vector<int64_t> sizes;
@@ -595,7 +596,13 @@ int pm_kd_shard_build(pm_kd_shard_plan* p, int32_t j, int32_t* d_tags, void* str
   hipError_t e;
   {
     PhaseTimer tm(PH_KDBUILD, s);
-    e = kd_shard_subtree(p->elems.p, p->sub.p, p->n, j, p->sizes[j], d_tags, s);
+    e = hipSuccess;
+    if (!p->boff.p) {
+      p->boff.alloc((size_t)kd_shard_tiles(p->n) * p->sizes.size());
+      e = p->boff.p ? kd_shard_offsets(p->sub.p, p->n, (int)p->sizes.size(), p->boff.p, s) : hipErrorOutOfMemory;
+      if (e != hipSuccess) p->boff.reset();
+    }
+    if (e == hipSuccess) e = kd_shard_subtree(p->elems.p, p->sub.p, p->boff.p, p->n, j, p->sizes[j], d_tags, s);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   return map_err(e);

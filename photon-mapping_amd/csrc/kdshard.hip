@@ -268,21 +268,59 @@ __global__ void k_shard_sub(const float4* __restrict__ elems, int64_t n, const f
   sub[i] = j < 0 ? 255 : (uint8_t)j;
 }
 
-__global__ void k_shard_flags(const uint8_t* __restrict__ sub, int64_t n, int j, uint32_t* __restrict__ flags) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  flags[i] = sub[i] == j ? 1u : 0u;
+// Subtree extraction. Once per plan, k_shard_count counts every subtree's
+// elements per tile of kShardExtTile and one scan over the (subtree, tile)
+// counts, subtree-major, gives each tile's start inside each subtree. A
+// subtree's extraction is then ONE pass: it reads the 1-B subtree ids and only
+// its own elements, ranks them inside the tile with wave ballots (chunk, wave,
+// lane order = index order: stable) and writes them out. The earlier per-subtree
+// flag / scan / extract passes moved ~21 B per element of the whole map for
+// every subtree a rank builds.
+constexpr int kShardExtTile = 4096;   // 256 threads x 16 chunks
+
+__global__ __launch_bounds__(256) void k_shard_count(const uint8_t* __restrict__ sub, int64_t n, int nb,
+                                                     int64_t tiles, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[32];
+  if (threadIdx.x < 32) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kShardExtTile;
+  for (int k = 0; k < kShardExtTile / 256; k++) {
+    const int64_t e = base + k * 256 + threadIdx.x;
+    if (e < n) {
+      const int b = sub[e];
+      if (b < nb) atomicAdd(&h[b], 1u);
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nb) cnt[threadIdx.x * tiles + blockIdx.x] = h[threadIdx.x];
 }
 
-__global__ void k_shard_extract(const float4* __restrict__ elems, int64_t n, const uint32_t* __restrict__ flags,
-                                const uint32_t* __restrict__ pos, float4* __restrict__ sub,
-                                int32_t* __restrict__ gid) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !flags[i]) return;
-  const float4 e = elems[i];
-  const uint32_t p = pos[i];
-  sub[p] = make_float4(e.x, e.y, e.z, __int_as_float((int)p));
-  gid[p] = __float_as_int(e.w);
+__global__ __launch_bounds__(256) void k_shard_extract(const float4* __restrict__ elems,
+                                                       const uint8_t* __restrict__ subof, int64_t n, int j,
+                                                       int64_t tiles, const uint32_t* __restrict__ boff,
+                                                       float4* __restrict__ sub, int32_t* __restrict__ gid) {
+  __shared__ uint32_t wc[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t run = boff[(int64_t)j * tiles + blockIdx.x] - boff[(int64_t)j * tiles];
+  const int64_t base = (int64_t)blockIdx.x * kShardExtTile;
+  for (int k = 0; k < kShardExtTile / 256; k++) {
+    const int64_t e = base + k * 256 + threadIdx.x;
+    const bool f = e < n && subof[e] == j;
+    const uint64_t m = __ballot(f);
+    if (lane == 0) wc[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int v = 0; v < w; v++) pre += wc[v];
+    const uint32_t tot = wc[0] + wc[1] + wc[2] + wc[3];
+    if (f) {
+      const uint32_t p = run + pre + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+      const float4 el = elems[e];
+      sub[p] = make_float4(el.x, el.y, el.z, __int_as_float((int)p));
+      gid[p] = __float_as_int(el.w);
+    }
+    run += tot;
+    __syncthreads();
+  }
 }
 
 // built subtree -> 4-B tags (original index << 2 | split dimension): the
@@ -673,18 +711,26 @@ hipError_t kd_shard_classify(const float4* elems, int64_t n, int L, const float4
   return hipGetLastError();
 }
 
-hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, int64_t n, int j, int64_t size,
-                            int32_t* out, hipStream_t s) {
+int64_t kd_shard_tiles(int64_t n) { return (n + kShardExtTile - 1) / kShardExtTile; }
+
+hipError_t kd_shard_offsets(const uint8_t* subof, int64_t n, int nb, uint32_t* boff, hipStream_t s) {
+  const int64_t tiles = kd_shard_tiles(n);
+  if (n <= 0 || nb < 1 || nb > 32 || tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
+  DevBuf<uint32_t> cnt(tiles * nb), total(1);
+  if (!cnt.p || !total.p) return hipErrorOutOfMemory;
+  k_shard_count<<<(int)tiles, 256, 0, s>>>(subof, n, nb, tiles, cnt.p);
+  PM_HIP_TRY(hipGetLastError());
+  return exclusive_scan_u32(cnt.p, boff, tiles * nb, total.p, s);
+}
+
+hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, const uint32_t* boff, int64_t n, int j,
+                            int64_t size, int32_t* out, hipStream_t s) {
   if (size <= 0) return hipSuccess;
-  DevBuf<uint32_t> flags(n), pos(n), total(1);
   DevBuf<float4> sub(size), nodes(size);
   DevBuf<int32_t> gid(size);
-  if (!flags.p || !pos.p || !total.p || !sub.p || !nodes.p || !gid.p) return hipErrorOutOfMemory;
-  const int g = grid_for(n, 256);
-  k_shard_flags<<<g, 256, 0, s>>>(subof, n, j, flags.p);
-  PM_HIP_TRY(hipGetLastError());
-  PM_HIP_TRY(exclusive_scan_u32(flags.p, pos.p, n, total.p, s));
-  k_shard_extract<<<g, 256, 0, s>>>(elems, n, flags.p, pos.p, sub.p, gid.p);
+  if (!sub.p || !nodes.p || !gid.p) return hipErrorOutOfMemory;
+  const int64_t tiles = kd_shard_tiles(n);
+  k_shard_extract<<<(int)tiles, 256, 0, s>>>(elems, subof, n, j, tiles, boff, sub.p, gid.p);
   PM_HIP_TRY(hipGetLastError());
   PM_HIP_TRY(kd_build(sub.p, size, nodes.p, s));
   k_shard_tags<<<grid_for(size, 256), 256, 0, s>>>(nodes.p, size, gid.p, out);

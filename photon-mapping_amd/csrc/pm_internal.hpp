@@ -91,8 +91,13 @@ bool shard_ok(int64_t n, int L);
 hipError_t kd_shard_top(const float4* elems, int64_t n, int L, float4* top, std::vector<int64_t>& sizes,
                         hipStream_t s);
 hipError_t kd_shard_classify(const float4* elems, int64_t n, int L, const float4* top, uint8_t* sub, hipStream_t s);
-hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, int64_t n, int j, int64_t size,
-                            int32_t* out, hipStream_t s);
+// Per-tile start of every subtree's elements (once per plan, nb = 2^L subtrees):
+// boff[j * tiles + t] = elements of subtrees < j, plus those of subtree j in
+// tiles < t (kShardExtTile elements per tile); sized by kd_shard_tiles.
+int64_t kd_shard_tiles(int64_t n);
+hipError_t kd_shard_offsets(const uint8_t* subof, int64_t n, int nb, uint32_t* boff, hipStream_t s);
+hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, const uint32_t* boff, int64_t n, int j,
+                            int64_t size, int32_t* out, hipStream_t s);
 hipError_t kd_shard_assemble(const float4* elems, const float4* top, int L, const int32_t* tags,
                              const std::vector<int64_t>& sizes, float4* nodes, hipStream_t s);
 struct ShardSel {
