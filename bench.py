@@ -11,7 +11,8 @@ Workload (BASELINE config 3): Sponza-class procedural scene (pm_amd.scenes,
 10M diffuse + 1M caustic photons per GPU, 1920x1080, spp 1, depth 30,
 k = 50, max_depth 10. value = emitted photons of the whole job / wall time of
 a step (Mphotons/s traced + gathered). N > 1: photon-index sharding with a
-single all-gather, replicated kd-tree build, 16x16-tile-sharded final gather,
+single all-gather, sharded kd-tree build (top levels selected from every
+rank's own photons, subtrees built per rank), 16x16-tile-sharded final gather,
 image reduce to rank 0 ("weak": photons per GPU fixed, config 4 at N = 8).
 --config 5: the caustics pass (square area light + glass, 6.25M caustic photons
 per GPU = 50M at N = 8, caustic gather over k = 200); the default line is config 3.
