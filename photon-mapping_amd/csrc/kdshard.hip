@@ -271,9 +271,10 @@ __global__ void k_shard_sub(const float4* __restrict__ elems, int64_t n, const f
 // Subtree extraction. Once per plan, k_shard_count counts every subtree's
 // elements per tile of kShardExtTile and one scan over the (subtree, tile)
 // counts, subtree-major, gives each tile's start inside each subtree. A
-// subtree's extraction is then ONE pass: it reads the 1-B subtree ids and only
-// its own elements, ranks them inside the tile with wave ballots (chunk, wave,
-// lane order = index order: stable) and writes them out. The earlier per-subtree
+// subtree's extraction is then ONE pass: it reads the 1-B subtree ids (16 per
+// thread, one 16-B load) and only its own elements, ranks them inside the tile
+// with a block scan of the per-thread match counts (thread order = index
+// order: stable) and writes them out. The earlier per-subtree
 // flag / scan / extract passes moved ~21 B per element of the whole map for
 // every subtree a rank builds.
 constexpr int kShardExtTile = 4096;   // 256 threads x 16 chunks
@@ -299,27 +300,41 @@ __global__ __launch_bounds__(256) void k_shard_extract(const float4* __restrict_
                                                        const uint8_t* __restrict__ subof, int64_t n, int j,
                                                        int64_t tiles, const uint32_t* __restrict__ boff,
                                                        float4* __restrict__ sub, int32_t* __restrict__ gid) {
-  __shared__ uint32_t wc[4];
+  // thread t owns elements [16 t, 16 t + 16) of the tile: one 16-B load of
+  // their subtree ids, a match mask, and a block scan of the match counts
+  __shared__ uint32_t wsum[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t run = boff[(int64_t)j * tiles + blockIdx.x] - boff[(int64_t)j * tiles];
-  const int64_t base = (int64_t)blockIdx.x * kShardExtTile;
-  for (int k = 0; k < kShardExtTile / 256; k++) {
-    const int64_t e = base + k * 256 + threadIdx.x;
-    const bool f = e < n && subof[e] == j;
-    const uint64_t m = __ballot(f);
-    if (lane == 0) wc[w] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t pre = 0;
-    for (int v = 0; v < w; v++) pre += wc[v];
-    const uint32_t tot = wc[0] + wc[1] + wc[2] + wc[3];
-    if (f) {
-      const uint32_t p = run + pre + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-      const float4 el = elems[e];
-      sub[p] = make_float4(el.x, el.y, el.z, __int_as_float((int)p));
-      gid[p] = __float_as_int(el.w);
-    }
-    run += tot;
-    __syncthreads();
+  const uint32_t run = boff[(int64_t)j * tiles + blockIdx.x] - boff[(int64_t)j * tiles];
+  const int64_t e0 = (int64_t)blockIdx.x * kShardExtTile + (int64_t)threadIdx.x * 16;
+  uint32_t wd[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};   // 255: matches no subtree
+  if (e0 + 16 <= n) {
+    const uint4 v = *reinterpret_cast<const uint4*>(subof + e0);
+    wd[0] = v.x, wd[1] = v.y, wd[2] = v.z, wd[3] = v.w;
+  } else {
+    for (int k = 0; k < 16 && e0 + k < n; k++)
+      wd[k >> 2] = (wd[k >> 2] & ~(0xFFu << (8 * (k & 3)))) | ((uint32_t)subof[e0 + k] << (8 * (k & 3)));
+  }
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) m |= (((wd[k >> 2] >> (8 * (k & 3))) & 0xFFu) == (uint32_t)j ? 1u : 0u) << k;
+  const uint32_t c = (uint32_t)__popc(m);
+  uint32_t x = c;   // inclusive wave scan
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t p = run + x - c;
+  for (int v = 0; v < w; v++) p += wsum[v];
+  while (m) {
+    const int k = __ffs(m) - 1;
+    m &= m - 1;
+    const float4 el = elems[e0 + k];
+    sub[p] = make_float4(el.x, el.y, el.z, __int_as_float((int)p));
+    gid[p] = __float_as_int(el.w);
+    p++;
   }
 }
 
