@@ -103,6 +103,25 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
     }
 
 
+def source_digest():
+    """sha256 over the library's sources (photon-mapping_amd/csrc, its Makefile,
+    include/pm.h): the identity of the code a PMC profile was collected on. The
+    built .so is not bit-reproducible across rebuilds (hipcc embeds per-build
+    ids in the code objects), so a rebuild of the same sources must not drop
+    roofline.traffic; an edited kernel changes this digest and does."""
+    import hashlib
+    h = hashlib.sha256()
+    pkg = os.path.join(ROOT, "photon-mapping_amd")
+    files = [os.path.join(pkg, "Makefile"), os.path.join(ROOT, "include", "pm.h")]
+    for d, _, fs in os.walk(os.path.join(pkg, "csrc")):
+        files += [os.path.join(d, f) for f in fs if f.endswith((".hip", ".hpp", ".cpp", ".h"))]
+    for f in sorted(files):
+        h.update(os.path.relpath(f, ROOT).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def secondary_config2(args):
     """The Cornell-box line (config 2, north_star's second workload) measured in a
     child process (its own device buffers and scene; this process's stay
@@ -273,8 +292,9 @@ def main():
             with open(pm_amd.LIB_PATH, "rb") as f:
                 lib_sha = hashlib.sha256(f.read()).hexdigest()
             # only while the library is the one the counters were collected on
+            # (the same binary, or a build of the same sources)
             if pmc.get("workload") == [args.scene, args.casted, args.caustic, args.width, args.height, args.spp] \
-                    and pmc.get("lib_sha256") == lib_sha:
+                    and (pmc.get("lib_sha256") == lib_sha or pmc.get("src_sha256") == source_digest()):
                 traffic = pmc.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None

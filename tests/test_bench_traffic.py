@@ -1,0 +1,33 @@
+"""bench.py's roofline.traffic identity: the PMC file is
+accepted for the built library's binary sha or for the digest of the sources it
+was built from, since hipcc builds are not bit-reproducible. CPU only."""
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _copy_tree(dst):
+    for rel in ("photon-mapping_amd/csrc", ):
+        shutil.copytree(os.path.join(ROOT, rel), os.path.join(dst, rel))
+    os.makedirs(os.path.join(dst, "include"))
+    shutil.copy(os.path.join(ROOT, "photon-mapping_amd", "Makefile"), os.path.join(dst, "photon-mapping_amd"))
+    shutil.copy(os.path.join(ROOT, "include", "pm.h"), os.path.join(dst, "include"))
+
+
+def test_source_digest_tracks_the_sources(tmp_path, monkeypatch):
+    import bench
+    d0 = bench.source_digest()
+    assert len(d0) == 64 and d0 == bench.source_digest()
+    _copy_tree(str(tmp_path))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.source_digest() == d0            # same sources elsewhere: same identity
+    knn = tmp_path / "photon-mapping_amd" / "csrc" / "knn.hip"
+    knn.write_bytes(knn.read_bytes() + b"\n// edited\n")
+    assert bench.source_digest() != d0            # an edited kernel drops the old counters
+    (tmp_path / "photon-mapping_amd" / "csrc" / "notes.txt").write_text("x")
+    d1 = bench.source_digest()
+    (tmp_path / "photon-mapping_amd" / "csrc" / "notes.txt").write_text("y")
+    assert bench.source_digest() == d1            # non-source files do not count

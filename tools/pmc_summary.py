@@ -19,6 +19,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import source_digest  # noqa: E402  (the identity bench.py checks)
 
 
 def pmc_table(path):
@@ -62,6 +64,7 @@ def main(tag="r01", src=os.path.join(ROOT, "gpurun_out", "prof"), workload=None)
         fetch, write = tot("FETCH_SIZE"), tot("WRITE_SIZE")
         with open(os.path.join(dst, "pmc_gather_global.json"), "w") as f:
             json.dump({"kernel": " + ".join(sorted(g)), "workload": workload, "tag": tag, "lib_sha256": lib_sha,
+                       "src_sha256": source_digest(),
                        "fetch_kib": fetch, "write_kib": write,
                        "hbm_bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None
                        else None,
