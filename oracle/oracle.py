@@ -98,6 +98,8 @@ def _load():
         "orc_map_create": (C.c_int, [_P, C.c_int64, C.c_float, _P, C.c_int64, C.c_float, C.POINTER(_P)]),
         "orc_map_destroy": (None, [_P]),
         "orc_set_build_threads": (None, [C.c_int32]),
+        "orc_kd_left_balanced": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int32, _P]),
+        "orc_left_size": (C.c_int64, [C.c_int64]),
         "orc_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_float, C.c_int32, _P, _P, _P]),
         "orc_gather": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, _P]),
         "orc_gather_k": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P]),
@@ -250,6 +252,23 @@ class PhotonMap:
         if getattr(self, "h", None):
             lib.orc_map_destroy(self.h)
             self.h = None
+
+
+def kd_left_balanced(pos: np.ndarray, nthreads: int = 8) -> np.ndarray:
+    """cukd::buildTree's left-balanced layout (ray-tracer/src/hostCode.cu:94-95):
+    int32 tag per node, original index << 2 | split dimension. `pos` is (n, >=3)
+    float32; columns 0..2 are the point."""
+    pos = np.ascontiguousarray(pos, np.float32)
+    n = len(pos)
+    tags = np.zeros((max(1, n),), np.int32)
+    stride = pos.shape[1] if pos.ndim == 2 else 3
+    _chk(lib.orc_kd_left_balanced(pos.ctypes.data if n else None, stride, n, int(nthreads),
+                                  tags.ctypes.data), "kd_left_balanced")
+    return tags[:n]
+
+
+def left_size(s: int) -> int:
+    return int(lib.orc_left_size(int(s)))
 
 
 def camera_setup(look_from, look_at, look_up, fovy, w, h) -> Camera:

@@ -799,6 +799,126 @@ void orc_map_destroy(orc_map* m) {
   free(m);
 }
 
+/* ------------------------------------------------------------------------ */
+/* cukd::buildTree<Photon, Photon_traits> layout (ray-tracer/src/hostCode.cu:
+ * 94-95; traits ray-tracer/include/photon.h:23-40, has_explicit_dim), restated
+ * as the build rules DESIGN.md §4.3 fixes (cudaKDTree is an empty submodule in
+ * the reference, so its published rules are what is restated):
+ *   - the tree is the implicit complete binary tree, children 2t+1 / 2t+2, over
+ *     the n records in place; subtree t holds s elements, its root the element
+ *     of rank left_size(s) (complete-tree left subtree size), the left child the
+ *     ls smaller elements, the right child the rest;
+ *   - order along dimension d = (orderable float key of coordinate d, original
+ *     index): -0.0 and +0.0 are one key, NaN is taken as +inf (include/pm.h);
+ *   - split dimension = the widest extent max - min (f32, from the subtree's
+ *     smallest and largest key), first dimension on a tie; written per node
+ *     (Photon_traits::set_dim, photon.h:36-39).
+ * This is an independent recursive restatement (quickselect per subtree), not
+ * the HIP level-by-level build; node t's output tag is orig << 2 | dim. */
+typedef struct { uint32_t k[3]; int32_t id; } lb_elem;
+
+static inline uint32_t lb_key(float f) {
+  if (f != f) f = INFINITY;
+  if (f == 0.0f) f = 0.0f;
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+static inline float lb_unkey(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+static inline uint64_t lb_ord(const lb_elem* e, int d) { return (uint64_t)e->k[d] << 32 | (uint32_t)e->id; }
+
+int64_t orc_left_size(int64_t s) {
+  if (s <= 1) return 0;
+  int h = 0;
+  while (((int64_t)1 << h) <= s) h++;            /* levels */
+  const int64_t half = (int64_t)1 << (h - 2);     /* left subtree's last-level capacity */
+  const int64_t full = ((int64_t)1 << (h - 1)) - 1;
+  const int64_t last = s - full;
+  return (half - 1) + (last < half ? last : half);
+}
+
+/* v[0..n): v[k] = rank-k element in (key d, index) order, smaller ones before it */
+static void lb_select(lb_elem* v, int64_t n, int64_t k, int d) {
+  int64_t lo = 0, hi = n - 1;
+  while (hi > lo) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    const uint64_t a = lb_ord(&v[lo], d), b = lb_ord(&v[mid], d), c = lb_ord(&v[hi], d);
+    const uint64_t pv = a < b ? (b < c ? b : (a < c ? c : a)) : (a < c ? a : (b < c ? c : b));
+    int64_t i = lo, j = hi;
+    while (i <= j) {
+      while (lb_ord(&v[i], d) < pv) i++;
+      while (pv < lb_ord(&v[j], d)) j--;
+      if (i <= j) {
+        const lb_elem t = v[i]; v[i] = v[j]; v[j] = t;
+        i++; j--;
+      }
+    }
+    if (k <= j) hi = j;
+    else if (k >= i) lo = i;
+    else return;
+  }
+}
+
+typedef struct { lb_elem* e; int32_t* tags; int64_t t, lo, hi; int par; } lb_task;
+static void lb_build(lb_elem* e, int32_t* tags, int64_t t, int64_t lo, int64_t hi, int par);
+static void* lb_thread(void* arg) {
+  lb_task* k = (lb_task*)arg;
+  lb_build(k->e, k->tags, k->t, k->lo, k->hi, k->par);
+  return NULL;
+}
+static void lb_build(lb_elem* e, int32_t* tags, int64_t t, int64_t lo, int64_t hi, int par) {
+  for (;;) {
+    const int64_t s = hi - lo;
+    if (s <= 0) return;
+    uint32_t mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
+    for (int64_t i = lo; i < hi; i++)
+      for (int d = 0; d < 3; d++) {
+        const uint32_t k = e[i].k[d];
+        if (k < mn[d]) mn[d] = k;
+        if (k > mx[d]) mx[d] = k;
+      }
+    float ext[3];
+    for (int d = 0; d < 3; d++) ext[d] = lb_unkey(mx[d]) - lb_unkey(mn[d]);
+    int dim = 0;
+    if (ext[1] > ext[dim]) dim = 1;
+    if (ext[2] > ext[dim]) dim = 2;
+    const int64_t ls = orc_left_size(s);
+    lb_select(&e[lo], s, ls, dim);
+    tags[t] = (int32_t)((uint32_t)e[lo + ls].id << 2 | (uint32_t)dim);
+    if (par > 1 && s > 65536) {
+      lb_task k = {e, tags, 2 * t + 1, lo, lo + ls, par / 2};
+      pthread_t th;
+      if (pthread_create(&th, NULL, lb_thread, &k) == 0) {
+        lb_build(e, tags, 2 * t + 2, lo + ls + 1, hi, par - par / 2);
+        pthread_join(th, NULL);
+        return;
+      }
+    }
+    lb_build(e, tags, 2 * t + 1, lo, lo + ls, 1);
+    t = 2 * t + 2;   /* right subtree: iterate */
+    lo = lo + ls + 1;
+  }
+}
+
+int orc_kd_left_balanced(const float* pos, int64_t stride, int64_t n, int32_t nthreads, int32_t* tags) {
+  if (n < 0 || stride < 3 || (n > 0 && (!pos || !tags)) || n >= ((int64_t)1 << 30)) return PM_ERR_INVALID;
+  if (n == 0) return PM_OK;
+  lb_elem* e = (lb_elem*)malloc(sizeof(lb_elem) * (size_t)n);
+  if (!e) return PM_ERR_INVALID;
+  for (int64_t i = 0; i < n; i++) {
+    for (int d = 0; d < 3; d++) e[i].k[d] = lb_key(pos[i * stride + d]);
+    e[i].id = (int32_t)i;
+  }
+  lb_build(e, tags, 0, 0, n, nthreads < 1 ? 1 : (nthreads > 256 ? 256 : nthreads));
+  free(e);
+  return PM_OK;
+}
+
 typedef struct { float d2; int32_t id; } cand;
 static inline int cand_less(cand a, cand b) { return a.d2 < b.d2 || (a.d2 == b.d2 && a.id < b.id); }
 typedef struct { cand* h; int k, cnt; float r2; } heap_t;

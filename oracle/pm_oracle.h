@@ -60,6 +60,12 @@ int orc_trace_photon_range(const orc_scene* s, const pm_light* lights, int32_t n
                            int64_t* count);
 
 /* --- stage 2 --- */
+/* cukd::buildTree's in-place left-balanced layout (ray-tracer/src/hostCode.cu:
+ * 94-95): tags[t] = original index << 2 | split dim of node t
+ * of the implicit tree over n points (pos: x, y, z at pos[i*stride]). */
+int orc_kd_left_balanced(const float* pos, int64_t stride, int64_t n, int32_t nthreads, int32_t* tags);
+/* complete-tree left subtree size of a subtree of s nodes */
+int64_t orc_left_size(int64_t s);
 /* threads used by orc_map_create's kd build (default 1) */
 void orc_set_build_threads(int32_t n);
 int orc_map_create(const pm_photon* a, int64_t na, float power_a,

@@ -599,7 +599,7 @@ int pm_kd_shard_build(pm_kd_shard_plan* p, int32_t j, int32_t* d_tags, void* str
     e = hipSuccess;
     if (!p->boff.p) {
       p->boff.alloc((size_t)kd_shard_tiles(p->n) * p->sizes.size());
-      e = p->boff.p ? kd_shard_offsets(p->sub.p, p->n, (int)p->sizes.size(), p->boff.p, s) : hipErrorOutOfMemory;
+      e = p->boff.p ? kd_shard_offsets(p->sub.p, p->n, (int)p->sizes.size(), p->sizes.data(), p->boff.p, s) : hipErrorOutOfMemory;
       if (e != hipSuccess) p->boff.reset();
     }
     if (e == hipSuccess) e = kd_shard_subtree(p->elems.p, p->sub.p, p->boff.p, p->n, j, p->sizes[j], d_tags, s);

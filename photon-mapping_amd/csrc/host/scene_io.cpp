@@ -27,6 +27,7 @@
 #include <deque>
 #include <fstream>
 #include <map>
+#include <set>
 #include <memory>
 #include <iterator>
 #include <sstream>
@@ -493,6 +494,9 @@ struct FbxReader {
       if ((size_t)n * es != clen) return false;
       raw.assign(b.data() + p, clen);
     } else if (enc == 1) {
+      // zlib cannot expand by more than ~1032:1: a header asking for more is
+      // malformed (and would otherwise allocate up to 32 GB from a tiny file)
+      if ((size_t)n * es > (size_t)clen * 1032 + 64) return false;
       raw.resize((size_t)n * es);
       uLongf dl = (uLongf)raw.size();
       if (uncompress((Bytef*)&raw[0], &dl, (const Bytef*)b.data() + p, clen) != Z_OK || dl != raw.size()) return false;
@@ -644,18 +648,27 @@ bool load_fbx(const std::string& path, RawScene& sc, std::string& err) {
   // model -> its geometries / materials / child models, in connection order
   std::map<int64_t, std::vector<int64_t>> mgeo, mmat, mkids;
   std::vector<int64_t> roots;
+  std::map<int64_t, int> nparents;
   for (const auto& [ch, par] : oo) {
     if (geoms.count(ch) && models.count(par)) mgeo[par].push_back(ch);
     else if (mats.count(ch) && models.count(par)) mmat[par].push_back(ch);
     else if (models.count(ch)) {
       if (par == 0) roots.push_back(ch);
       else if (models.count(par)) mkids[par].push_back(ch);
+      else continue;
+      // a node hierarchy is a tree (as load_glb requires): one parent per model
+      if (++nparents[ch] > 1) { err = "FBX model " + std::to_string(ch) + " has two parents"; return false; }
     }
   }
   static const char* complex[] = {"RotationOffset", "RotationPivot", "PreRotation", "PostRotation", "ScalingOffset",
                                   "ScalingPivot", "GeometricTranslation", "GeometricRotation", "GeometricScaling"};
   std::map<int64_t, int> node_of;
+  std::set<int64_t> on_path;   // models being built: reaching one again is a cycle
   std::function<int(int64_t)> build_node = [&](int64_t id) -> int {
+    if (!on_path.insert(id).second || node_of.count(id)) {
+      err = "FBX model hierarchy has a cycle through model " + std::to_string(id);
+      return -1;
+    }
     const FbxNode& m = *models.at(id);
     const auto P = fbx_p70(m);
     for (const char* c : complex) {
@@ -725,7 +738,8 @@ bool load_fbx(const std::string& path, RawScene& sc, std::string& err) {
       for (int mi : order) {
         RawMesh rm;
         const auto& ml = mmat[id];
-        rm.material = (mi >= 0 && mi < (int)ml.size()) ? fbx_name(mats.at(ml[mi])->props[1].str) : "DefaultMaterial";
+        const FbxNode* mat = (mi >= 0 && mi < (int)ml.size()) ? mats.at(ml[mi]) : nullptr;
+        rm.material = mat && mat->props.size() >= 2 ? fbx_name(mat->props[1].str) : "DefaultMaterial";
         for (size_t k = 0; k < polys.size(); k++) {
           if (pmat[k] != mi || polys[k].size() < 3) continue;
           const int base = (int)rm.pos.size();
@@ -766,6 +780,7 @@ bool load_fbx(const std::string& path, RawScene& sc, std::string& err) {
       if (c < 0) return -1;
       sc.nodes[me].children.push_back(c);
     }
+    on_path.erase(id);
     return me;
   };
   RawNode root;
@@ -807,7 +822,23 @@ struct pm_scene_data {
   int64_t nv = 0, nt = 0;
 };
 
+static int scene_data_load(const char* cpath, pm_scene_data** out);
+
+// No C++ exception crosses the C ABI: an allocation failure or a malformed file
+// that a parser step did not anticipate becomes PM_ERR_IO.
 extern "C" int pm_scene_data_load(const char* cpath, pm_scene_data** out) {
+  try {
+    return scene_data_load(cpath, out);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "pm: scene import failed: %s\n", e.what());
+  } catch (...) {
+    std::fprintf(stderr, "pm: scene import failed: unknown error\n");
+  }
+  if (out) *out = nullptr;
+  return PM_ERR_IO;
+}
+
+static int scene_data_load(const char* cpath, pm_scene_data** out) {
   if (!cpath || !out) return PM_ERR_INVALID;
   *out = nullptr;
   const std::string path = native(cpath);

@@ -728,14 +728,28 @@ hipError_t kd_shard_classify(const float4* elems, int64_t n, int L, const float4
 
 int64_t kd_shard_tiles(int64_t n) { return (n + kShardExtTile - 1) / kShardExtTile; }
 
-hipError_t kd_shard_offsets(const uint8_t* subof, int64_t n, int nb, uint32_t* boff, hipStream_t s) {
+// `expect`: the plan's subtree sizes. k_shard_extract writes each subtree's
+// elements into a buffer of exactly that size, so the counts found here must
+// agree: a plan whose sizes came from a distributed selection fed the wrong
+// reductions (pm_kd_shard_plan_create_from_sel) is refused with
+// hipErrorInvalidValue instead of writing past a subtree buffer.
+hipError_t kd_shard_offsets(const uint8_t* subof, int64_t n, int nb, const int64_t* expect, uint32_t* boff,
+                            hipStream_t s) {
   const int64_t tiles = kd_shard_tiles(n);
-  if (n <= 0 || nb < 1 || nb > 32 || tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
+  if (n <= 0 || nb < 1 || nb > 32 || tiles > 0x7FFFFFFF || tiles * nb > 0xFFFFFFFFll) return hipErrorInvalidValue;
   DevBuf<uint32_t> cnt(tiles * nb), total(1);
   if (!cnt.p || !total.p) return hipErrorOutOfMemory;
   k_shard_count<<<(int)tiles, 256, 0, s>>>(subof, n, nb, tiles, cnt.p);
   PM_HIP_TRY(hipGetLastError());
-  return exclusive_scan_u32(cnt.p, boff, tiles * nb, total.p, s);
+  PM_HIP_TRY(exclusive_scan_u32(cnt.p, boff, tiles * nb, total.p, s));
+  uint32_t start[33];
+  for (int j = 0; j < nb; j++)
+    PM_HIP_TRY(hipMemcpyAsync(&start[j], boff + (int64_t)j * tiles, 4, hipMemcpyDeviceToHost, s));
+  PM_HIP_TRY(hipMemcpyAsync(&start[nb], total.p, 4, hipMemcpyDeviceToHost, s));
+  PM_HIP_TRY(hipStreamSynchronize(s));
+  for (int j = 0; j < nb; j++)
+    if ((int64_t)(start[j + 1] - start[j]) != expect[j]) return hipErrorInvalidValue;
+  return hipSuccess;
 }
 
 hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, const uint32_t* boff, int64_t n, int j,

@@ -95,7 +95,8 @@ hipError_t kd_shard_classify(const float4* elems, int64_t n, int L, const float4
 // boff[j * tiles + t] = elements of subtrees < j, plus those of subtree j in
 // tiles < t (kShardExtTile elements per tile); sized by kd_shard_tiles.
 int64_t kd_shard_tiles(int64_t n);
-hipError_t kd_shard_offsets(const uint8_t* subof, int64_t n, int nb, uint32_t* boff, hipStream_t s);
+hipError_t kd_shard_offsets(const uint8_t* subof, int64_t n, int nb, const int64_t* expect, uint32_t* boff,
+                            hipStream_t s);
 hipError_t kd_shard_subtree(const float4* elems, const uint8_t* subof, const uint32_t* boff, int64_t n, int j,
                             int64_t size, int32_t* out, hipStream_t s);
 hipError_t kd_shard_assemble(const float4* elems, const float4* top, int L, const int32_t* tags,

@@ -10,6 +10,10 @@ oracle finishes in seconds.
     frame's own queries per map, sampled uniformly, must carry bit for bit the
     radiance the oracle's gatherPhotons (shading.h:93-121, over an independent
     exact kNN, shading.h:11-18) computes on maps built from the same photons.
+  - kd layout: both maps' trees node for node against the oracle's
+    restatement of cukd's left-balanced layout (tests/kd_layout.py);
+  - image: a 48-row band at the frame centre rendered by the oracle over the
+    full maps, L_inf <= 1e-3 and >= 99.9 % of pixels bitwise vs the HIP frame.
 The GPU photons the maps are built from are the ones the frame used (their
 bitwise agreement with the oracle is the trace check above and, at reduced
 size, test_gpu_workloads.py)."""
@@ -17,12 +21,14 @@ import numpy as np
 import pytest
 
 import conftest
+import kd_layout
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 NT = conftest.ORACLE_THREADS
 CAM = ((80.0, 30.0, 0.0), (10.0, 20.0, 0.0), (0.0, 1.0, 0.0), 0.87)
 SAMPLE = 50_000
+BAND = 48
 
 
 def _bits(a):
@@ -39,32 +45,57 @@ def _trace_shards_vs_oracle(gs, os_, lights, casted, caustics):
         assert np.array_equal(_bits(g.cpu().numpy()), _bits(o)), (rank, caustics)
 
 
-def _frame_gathers_vs_oracle(gs, lights, g, c, caustic_k, W=1920, H=1080):
+def _frame_vs_oracle(gs, os_, lights, g, c, caustic_k, W=1920, H=1080):
     import oracle
     import pm_amd
     gm, cm = pm_amd.load_photons(g, c)
+    og, oc = g.cpu().numpy(), c.cpu().numpy()
+    # the two kd-trees node for node against the oracle's left-balanced layout
+    # (cukd::buildTree, ray-tracer/src/hostCode.cu:94-95; the global map is
+    # built by the selection build at this size)
+    for m, parts, what in ((gm, [(og, 1.0), (oc, 0.5)], "global"), (cm, [(oc, 0.5)], "caustic")):
+        want, _ = kd_layout.map_records(parts, NT)
+        kd_layout.assert_same(m.export().cpu().numpy(), want, what)
+        del want
     cam = pm_amd.setup_camera(*CAM, W, H)
     job = pm_amd.render_begin(gs, cam, W, H, 1, 30, (1, 1, 1), lights, caustic_k=caustic_k)
-    job.finish(gm, cm, want_rgb=False)
+    rgba, rgb = job.finish(gm, cm)
+    rgb = rgb.cpu().numpy()
     st = pm_amd.render_stats()
-    og, oc = g.cpu().numpy(), c.cpu().numpy()
     rng = np.random.default_rng(2024)
     checked = {}
+    om = {"global": oracle.PhotonMap(og, 1.0, oc, 0.5, nthreads=NT), "caustic": oracle.PhotonMap(oc, 0.5, nthreads=NT)}
     for which, k in (("global", 50), ("caustic", caustic_k or 50)):
         q, r = job.queries(which)
         n = q.shape[0]
         assert n == (st.global_queries if which == "global" else st.caustic_queries)
         idx = torch.from_numpy(np.sort(rng.choice(n, size=min(SAMPLE, n), replace=False))).cuda()
         qs, rs = q[idx].cpu().numpy(), r[idx].cpu().numpy()
-        om = oracle.PhotonMap(og, 1.0, oc, 0.5, nthreads=NT) if which == "global" else \
-            oracle.PhotonMap(oc, 0.5, nthreads=NT)
         pts = np.ascontiguousarray(qs[:, 0:3])
-        want = om.gather(pts, np.ascontiguousarray(qs[:, 3]), nthreads=NT, k=k)
+        want = om[which].gather(pts, np.ascontiguousarray(qs[:, 3]), nthreads=NT, k=k)
         assert np.array_equal(_bits(rs[:, 0:3]), _bits(want)), which
         assert np.count_nonzero(want) > 0.05 * want.size, which   # lit queries, not an all-zero comparison
         checked[which] = n
-        del om
     job.close()
+    # a BAND-row strip of the full-resolution frame at its centre, rendered by the
+    # oracle over the full maps (simpleRayGen, ray-tracer/cuda/deviceCode.cu:
+    # 191-231: camera paths, direct light, caustic gather, 20 final-gather rays
+    # per vertex, the framebuffer row H - y written at :229-230)
+    lo = H // 2 - BAND // 2
+    ocam = oracle.camera_setup(*CAM, W, H)
+    orgba, orgb, ost = oracle.render(os_, ocam, W, H, 1, 30, (1, 1, 1), lights, om["global"], om["caustic"],
+                                     rows=(lo, lo + BAND), nthreads=NT, caustic_k=caustic_k)
+    rows = slice(H - (lo + BAND) + 1, H - lo + 1)
+    a, b = np.clip(rgb[rows], 0, 1), np.clip(orgb[rows], 0, 1)
+    err = float(np.abs(a - b).max())
+    exact = float(np.mean(np.all(_bits(rgb[rows]) == _bits(orgb[rows]), axis=-1)))
+    assert ost.pixels == BAND * W
+    assert err <= 1e-3, err
+    assert exact >= 0.999, exact
+    assert np.mean(rgba.cpu().numpy().view(np.uint32)[rows] != orgba[rows]) <= 0.001
+    assert np.mean(orgb[rows]) > 0.01   # a lit band, not an all-black comparison
+    checked["band_exact"] = exact
+    del om
     return st, checked, gm.n, cm.n
 
 
@@ -80,7 +111,7 @@ def test_config3_full_size_vs_oracle():
     _trace_shards_vs_oracle(gs, os_, lights, 1_000_000, True)
     g = pm_amd.run_normal(gs, lights, 10_000_000, 10)
     c = pm_amd.run_caustics(gs, lights, 1_000_000, 10)
-    st, checked, ng, nc = _frame_gathers_vs_oracle(gs, lights, g, c, 0)
+    st, checked, ng, nc = _frame_vs_oracle(gs, os_, lights, g, c, 0)
     assert ng > 40_000_000 and checked["global"] > 30_000_000, (ng, checked)
 
 
@@ -96,5 +127,5 @@ def test_config5_full_size_vs_oracle():
     _trace_shards_vs_oracle(gs, os_, lights, 6_250_000, True)
     g = pm_amd.run_normal(gs, lights, 10_000_000, 10)
     c = pm_amd.run_caustics(gs, lights, 6_250_000, 10)
-    st, checked, ng, nc = _frame_gathers_vs_oracle(gs, lights, g, c, 200)
+    st, checked, ng, nc = _frame_vs_oracle(gs, os_, lights, g, c, 200)
     assert nc > 500_000 and checked["caustic"] > 2_000_000, (nc, checked)

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import conftest
+import kd_layout
 
 pytestmark = pytest.mark.gpu
 
@@ -179,6 +180,9 @@ def test_kdtree_build_left_balanced(n):
     o2[:, 10] = 0
     assert np.array_equal(rec[key(rec)][:, :10].view(np.uint32), o2[key(o2)][:, :10].view(np.uint32))
     _check_left_balanced(out[:, :3], dims.astype(np.int64))
+    # node for node against the oracle's restatement of the layout
+    want, _ = kd_layout.inplace_records(rec, conftest.ORACLE_THREADS)
+    kd_layout.assert_same(out, want, f"pm_kdtree_build n={n}")
 
 
 def _brute_knn(pts, q, k, r):
@@ -271,6 +275,11 @@ def test_photon_map_export(cornell):
     dims = e[:, 10].view(np.uint32) >> 24
     _check_left_balanced(e[:, :3], dims.astype(np.int64))
     assert np.all(e[:, 9] == 1.0)
+    kd_layout.assert_same(e, kd_layout.map_records([(g, 1.0)])[0], "export")
+    # two photon sets (loadPhotons: diffuse ++ caustic, powers 1 / 0.5)
+    c = oracle.trace(oracle.Scene(meshes), lights, 5000, 10, True)
+    m2 = pm_amd.PhotonMap(torch.from_numpy(g).cuda(), 1.0, torch.from_numpy(c).cuda(), 0.5)
+    kd_layout.assert_same(m2.export().cpu().numpy(), kd_layout.map_records([(g, 1.0), (c, 0.5)])[0], "export a++b")
 
 
 def _render_pair(meshes, lights, casted, W, H, spp, tiles=(0, 1), caustic_k=0):
@@ -500,6 +509,10 @@ def test_sharded_kd_build_equals_replicated(cornell, world, data):
     m = pmdist.shard_assemble(plan, torch.cat(bufs), world)
     assert m.n == ref.n
     assert torch.equal(m.export().view(torch.int32), ref.export().view(torch.int32))
+    if world == 2:   # the one-device tree itself against the oracle's layout
+        want, _ = kd_layout.map_records([(g.cpu().numpy(), pm_amd.PHOTON_POWER),
+                                         (c.cpu().numpy(), pm_amd.CAUSTICS_PHOTON_POWER)])
+        kd_layout.assert_same(ref.export().cpu().numpy(), want, f"map ({data})")
     rng = np.random.default_rng(3)
     q = torch.from_numpy(rng.uniform(-20, 20, size=(3000, 3)).astype(np.float32)).cuda()
     brdf = torch.from_numpy(rng.uniform(0, 0.4, size=3000).astype(np.float32)).cuda()
@@ -641,3 +654,22 @@ def test_nan_positions_build_as_inf(cornell):
     out = tr.cpu().numpy()
     pos = np.where(np.isnan(out[:, 0:3]), np.inf, out[:, 0:3])
     _check_left_balanced(pos, (out[:, 10].view(np.uint32) >> 24).astype(np.int64))
+    kd_layout.assert_same(out, kd_layout.inplace_records(rec)[0], "in place, NaN as +inf")
+    kd_layout.assert_same(gm.export().cpu().numpy(), kd_layout.map_records([(gn, 1.0)])[0], "map, NaN as +inf")
+
+
+def test_shard_plan_from_mismatched_selection_is_refused():
+    """a plan whose subtree sizes come from a distributed selection
+    over OTHER photons (wrong offsets or reductions) must not extract past its
+    subtree buffers: the first pm_kd_shard_build checks the counted subtree
+    sizes against the plan's and returns PM_ERR_INVALID."""
+    import pm_amd
+    from pm_amd import dist as pmdist
+    g, c = _synthetic_photons(70001, 5), _synthetic_photons(999, 6)
+    sel, _ = pmdist.simulated_top_selection(pm_amd, g, c, 4)
+    g2 = g.flip(0).contiguous()   # the same points under other indices
+    g2[: len(g2) // 2, 0] += 7.0
+    plan = pm_amd.KdShardPlan(g2, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=4, sel=sel)
+    with pytest.raises(pm_amd.PMError) as e:
+        pmdist.shard_local(plan, 0, 4)
+    assert e.value.status == pm_amd.PM_ERR_INVALID

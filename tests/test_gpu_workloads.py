@@ -21,6 +21,7 @@ import numpy as np
 import pytest
 
 import conftest
+import kd_layout
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -75,8 +76,11 @@ def test_config2_cornell_full_size(cornell):
     """BASELINE config 2 exactly: Cornell, 1M + 1M photons, 512x512, spp 1."""
     meshes, lights = cornell
     gs, os_, g, c, og, oc = _trace_pair(meshes, lights, 1_000_000, 1_000_000)
-    _, _, _, _, st = _render_check(gs, os_, lights, g, c, og, oc, 512, 512)
+    gm, cm, _, _, st = _render_check(gs, os_, lights, g, c, og, oc, 512, 512)
     assert st.pixels == 512 * 512 and st.global_queries > 1_000_000
+    # both kd-trees node for node against the oracle's left-balanced layout
+    for m, parts, what in ((gm, [(og, 1.0), (oc, 0.5)], "global"), (cm, [(oc, 0.5)], "caustic")):
+        kd_layout.assert_same(m.export().cpu().numpy(), kd_layout.map_records(parts, NT)[0], what)
 
 
 def test_config3_sponza_class_reduced():

@@ -442,13 +442,24 @@ def test_fbx_hierarchy_materials_and_quads(tmp_path):
     assert np.array_equal(np.sort(meshes[5].vertices, 0), np.sort(f32(2 * (two[4:7] + [10, 0, 0])), 0))
 
 
-@pytest.mark.parametrize("bad", ["magic", "truncated", "array_len", "pivot"])
+@pytest.mark.parametrize("bad", ["magic", "truncated", "array_len", "pivot", "cycle", "two_parents", "zlib_bomb"])
 def test_malformed_fbx_rejected(tmp_path, bad):
+    """PM_ERR_IO, never a crash: bad magic, truncation, array lengths, pivots,
+    a model hierarchy that is not a tree (a cycle, a model with two parents;
+    load_glb rejects the same), a compressed array whose header asks for far
+    more than zlib can expand its payload to."""
     import pm_amd
     objects = _fbx_node("Objects", [], [_geometry(11, "g", TRI.astype(np.float64), [[0, 1, 2]]),
-                                        _model(21, "m", **({"RotationPivot": (1, 0, 0)} if bad == "pivot" else {}))])
-    conns = _fbx_node("Connections", [], [_fbx_node("C", ["OO", 21, 0]), _fbx_node("C", ["OO", 11, 21])])
+                                        _model(21, "m", **({"RotationPivot": (1, 0, 0)} if bad == "pivot" else {})),
+                                        _model(22, "k"), _model(23, "j")])
+    C = lambda a, b: _fbx_node("C", ["OO", a, b])
+    extra = {"cycle": [C(22, 21), C(23, 22), C(22, 23)], "two_parents": [C(22, 21), C(23, 21), C(23, 22)]}
+    conns = _fbx_node("Connections", [], [C(21, 0), C(11, 21)] + extra.get(bad, []))
     blob = _fbx_file([objects, conns])
+    if bad == "zlib_bomb":   # Vertices array: enc 1, 2^28 doubles claimed from its few payload bytes
+        i = blob.index(b"Vertices") + len(b"Vertices") + 1
+        n, enc, clen = struct.unpack("<III", blob[i:i + 12])
+        blob = blob[:i] + struct.pack("<III", 1 << 28, 1, clen) + blob[i + 12:]
     if bad == "magic":
         blob = b"Kaydara FBX Ascii   " + blob[20:]
     elif bad == "truncated":
@@ -461,3 +472,17 @@ def test_malformed_fbx_rejected(tmp_path, bad):
     with pytest.raises(pm_amd.PMError) as e:
         _load(str(tmp_path / "x.fbx"))
     assert e.value.status == pm_amd.PM_ERR_IO
+
+
+def test_fbx_short_material_record_falls_back(tmp_path):
+    """A Material record without its name property: the mesh takes
+    DefaultMaterial instead of reading past the record."""
+    objects = _fbx_node("Objects", [], [_geometry(11, "g", TRI.astype(np.float64), [[0, 1, 2]], mat=[0]),
+                                        _model(21, "m"), _fbx_node("Material", [31])])
+    C = lambda a, b: _fbx_node("C", ["OO", a, b])
+    conns = _fbx_node("Connections", [], [C(21, 0), C(11, 21), C(31, 21)])
+    (tmp_path / "x.fbx").write_bytes(_fbx_file([objects, conns]))
+    (tmp_path / "lights.txt").write_text("0 20 0 1 1 1 10\n")
+    meshes, _ = _load(str(tmp_path / "x.fbx"))
+    assert [m.name for m in meshes] == ["DefaultMaterial"]
+    assert np.allclose(meshes[0].material, DEFAULT_MAT)
