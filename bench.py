@@ -105,13 +105,24 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
 
 def source_digest():
     """sha256 over the library's sources (photon-mapping_amd/csrc, its Makefile,
-    include/pm.h): the identity of the code a PMC profile was collected on. The
-    built .so is not bit-reproducible across rebuilds (hipcc embeds per-build
-    ids in the code objects), so a rebuild of the same sources must not drop
-    roofline.traffic; an edited kernel changes this digest and does."""
+    include/pm.h) and the compile flags it was built with (build_flags.txt,
+    written by the Makefile beside the library in use: PM_HIP_LIB or lib/):
+    the identity of the code a PMC profile was collected on. The built .so is
+    not bit-reproducible across rebuilds (hipcc embeds per-build ids in the
+    code objects), so a rebuild of the same sources must not drop
+    roofline.traffic; an edited kernel, or a variant library built from the
+    same sources with other -D flags (make check / budget, tools/
+    build_variant.sh), changes this digest and does."""
     import hashlib
     h = hashlib.sha256()
     pkg = os.path.join(ROOT, "photon-mapping_amd")
+    lib = os.environ.get("PM_HIP_LIB") or os.path.join(pkg, "lib", "libpm_hip.so")
+    flags = os.path.join(os.path.dirname(os.path.abspath(lib)), "build_flags.txt")
+    if os.path.exists(flags):
+        with open(flags, "rb") as fh:
+            h.update(b"flags:" + b" ".join(fh.read().split()))
+    else:
+        h.update(b"flags:unknown")
     files = [os.path.join(pkg, "Makefile"), os.path.join(ROOT, "include", "pm.h")]
     for d, _, fs in os.walk(os.path.join(pkg, "csrc")):
         files += [os.path.join(d, f) for f in fs if f.endswith((".hip", ".hpp", ".cpp", ".h"))]
@@ -205,6 +216,7 @@ def main():
     backend_name = os.environ.get("PM_DIST_BACKEND", "nccl")
     torch.cuda.set_device(0 if backend_name == "gloo" else local_rank)
     dist = None
+    sel_group = None
     if world > 1:
         import torch.distributed as tdist
         if backend_name == "gloo":
@@ -213,6 +225,13 @@ def main():
         else:
             tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
             dist = tdist
+            # the distributed top selection's own communicator, made (and its
+            # first collective run) here, before any frame: its all-reduces run
+            # beside the photon all-gather of the default group
+            sel_group = tdist.new_group()
+            warm = torch.zeros(1, dtype=torch.int64, device="cuda")
+            tdist.all_reduce(warm, group=sel_group)
+            torch.cuda.synchronize()
 
     if args.scene == "sponza" and args.config == 5:
         meshes, lights = scenes.sponza_caustics()
@@ -249,7 +268,7 @@ def main():
         if not isinstance(getattr(cfg, field, None), bool) or v not in ("0", "1"):
             raise SystemExit(f"--frame-opt: {opt!r} is not FIELD=0|1 for a boolean FrameConfig field")
         setattr(cfg, field, v == "1")
-    backend = pmdist.GpuBackend(scene, lights, cfg, rank, world, gbuf=gbuf, cbuf=cbuf)
+    backend = pmdist.GpuBackend(scene, lights, cfg, rank, world, gbuf=gbuf, cbuf=cbuf, sel_group=sel_group)
 
     def step():
         _, fi = pmdist.frame(backend, rank, world, dist, rgba)

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 4
+#define PM_ABI_VERSION 5
 
 enum pm_status {
   PM_OK = 0,
@@ -208,6 +208,30 @@ typedef struct pm_photon_map pm_photon_map;
 int pm_photon_map_create(const pm_photon* d_a, int64_t na, float power_a,
                          const pm_photon* d_b, int64_t nb, float power_b,
                          pm_photon_map** out, void* stream);
+/* Photon ROWS: the photons of one set as nseg segments of row_floats-float
+ * rows in one device buffer, concatenated in segment order: segment s is rows
+ * [seg_row0[s], seg_row0[s] + seg_count[s]) of d_rows; the position is floats
+ * 0..2 of a row and the colour floats color_offset..color_offset+2. A
+ * pm_photon array is {10, 7, one segment}. The N > 1 exchange
+ * all-gathers (position, colour) rows padded to the largest rank's count into
+ * one buffer, rank r at rows [r m, r m + n_r): {6, 3, world segments} hands that
+ * buffer to the maps as it is, with no compaction and no re-expansion to
+ * pm_photon. Original index = position in the concatenation, as for the
+ * pm_photon calls (a ++ b). A NULL set has no photons. */
+#define PM_ROWS_MAX_SEGS 32
+typedef struct {
+  const float* d_rows;
+  int32_t row_floats;          /* >= 6 */
+  int32_t color_offset;        /* >= 3, color_offset + 3 <= row_floats */
+  int32_t nseg;                /* 0 .. PM_ROWS_MAX_SEGS */
+  int32_t reserved;            /* 0 */
+  int64_t seg_row0[PM_ROWS_MAX_SEGS];
+  int64_t seg_count[PM_ROWS_MAX_SEGS];
+} pm_photon_rows;
+/* pm_photon_map_create over photon rows (the same map as over the concatenated
+ * pm_photon arrays, bit for bit). */
+int pm_photon_map_create_rows(const pm_photon_rows* a, float power_a, const pm_photon_rows* b, float power_b,
+                              pm_photon_map** out, void* stream);
 int pm_photon_map_size(const pm_photon_map* map, int64_t* n);
 /* Copy the map out in kd order as reference kd records (power, split_dim set). */
 int pm_photon_map_export(const pm_photon_map* map, pm_kd_photon* d_out, void* stream);
@@ -235,6 +259,9 @@ int pm_kd_shard_build(pm_kd_shard_plan* plan, int32_t subtree, int32_t* d_tags /
 /* d_tags: all subtrees' tags in subtree order (NULL if count == 0). */
 int pm_photon_map_create_sharded(pm_kd_shard_plan* plan, const int32_t* d_tags,
                                  pm_photon_map** out, void* stream);
+/* pm_kd_shard_plan_create over photon rows (see pm_photon_rows). */
+int pm_kd_shard_plan_create_rows(const pm_photon_rows* a, float power_a, const pm_photon_rows* b, float power_b,
+                                 int32_t world, pm_kd_shard_plan** out, void* stream);
 int pm_kd_shard_plan_destroy(pm_kd_shard_plan* plan);
 
 /* Distributed top selection: the same top L levels and subtree sizes as
@@ -263,6 +290,10 @@ int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* sel,
                                      const pm_photon* d_a, int64_t na, float power_a,
                                      const pm_photon* d_b, int64_t nb, float power_b,
                                      pm_kd_shard_plan** out, void* stream);
+/* the same over the gathered photon rows (the exchange's padded buffer) */
+int pm_kd_shard_plan_create_from_sel_rows(const pm_kd_top_sel* sel, const pm_photon_rows* a, float power_a,
+                                          const pm_photon_rows* b, float power_b, pm_kd_shard_plan** out,
+                                          void* stream);
 int pm_kd_top_sel_destroy(pm_kd_top_sel* sel);
 
 /* ---- stage 2b: kNN + radiance estimate ----------------------------------

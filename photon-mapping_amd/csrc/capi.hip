@@ -30,8 +30,6 @@ hipError_t launch_trace_chunk(pm_scene* sc, const LightDev* d_lights, const int6
                               int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt, hipStream_t s);
 hipError_t launch_compact(const pm_photon* slots, const uint32_t* cnt, const uint32_t* off, int64_t np,
                           pm_photon* out, hipStream_t s);
-hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
-                                     float pb, float4* elems, float4* payload, hipStream_t s);
 hipError_t kd_build_records(pm_kd_photon* d, int64_t n, pm_box* bounds, hipStream_t s);
 hipError_t launch_map_export(const pm_photon_map* m, pm_kd_photon* out, hipStream_t s);
 hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, int k, float radius, int32_t* ids,
@@ -147,6 +145,36 @@ bool ptr_elsewhere(const void* p, int dev) {
     int _st = map_err(expr);        \
     if (_st != PM_OK) return _st;   \
   } while (0)
+
+// the runs of two pm_photon arrays (a ++ b)
+RowRuns runs_of(const pm_photon* a, int64_t na, float pa, const pm_photon* b, int64_t nb, float pb) {
+  RowRuns r;
+  if (na > 0) r.push_back({reinterpret_cast<const float*>(a), 10, 7, na, pa});
+  if (nb > 0) r.push_back({reinterpret_cast<const float*>(b), 10, 7, nb, pb});
+  return r;
+}
+
+// the runs of a pm_photon_rows set (NULL: none); false on a malformed descriptor
+bool runs_of_rows(const pm_photon_rows* x, float power, RowRuns& out) {
+  if (!x) return true;
+  if (x->nseg < 0 || x->nseg > PM_ROWS_MAX_SEGS || x->row_floats < 6 || x->color_offset < 3 ||
+      x->color_offset > x->row_floats - 3 || x->reserved != 0)
+    return false;
+  for (int k = 0; k < x->nseg; k++) {
+    if (x->seg_row0[k] < 0 || x->seg_count[k] < 0) return false;
+    if (x->seg_count[k] == 0) continue;
+    if (!x->d_rows) return false;
+    out.push_back({x->d_rows + x->seg_row0[k] * x->row_floats, x->row_floats, x->color_offset, x->seg_count[k], power});
+  }
+  return true;
+}
+
+// every run's rows on the call's device
+bool runs_elsewhere(const RowRuns& runs, int dev) {
+  for (const RowRun& r : runs)
+    if (ptr_elsewhere(r.rows, dev)) return true;
+  return false;
+}
 
 }  // namespace
 
@@ -448,18 +476,15 @@ int pm_kdtree_build(pm_kd_photon* d, int64_t n, pm_box* bounds, void* stream) {
   return map_err(kd_build_records(d, n, bounds, s));
 }
 
-int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_photon* b, int64_t nb, float pb,
-                         pm_photon_map** out, void* stream) {
-  if (!out || na < 0 || nb < 0 || (na > 0 && !a) || (nb > 0 && !b)) return PM_ERR_INVALID;
+static int map_create_runs(const RowRuns& runs, pm_photon_map** out, void* stream) {
   *out = nullptr;
-  const int64_t n = na + nb;
+  const int64_t n = rows_total(runs);
   if (n >= kMaxMapPhotons) return PM_ERR_INVALID;
   int st = require_device();
   if (st != PM_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
-  PM_PTR_DEVICE(alloc_scope, a);
-  PM_PTR_DEVICE(alloc_scope, b);
+  if (runs_elsewhere(runs, alloc_scope.dev)) return PM_ERR_DEVICE;
   pm_photon_map* m = new pm_photon_map;
   m->made_on = s;
   m->device = alloc_scope.dev;
@@ -476,7 +501,7 @@ int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_phot
     hipError_t e;
     {
       PhaseTimer tm(PH_KDBUILD, s);
-      e = launch_elems_from_photons(a, na, b, nb, pa, pb, elems.p, m->payload.p, s);
+      e = launch_elems_from_rows(runs, elems.p, m->payload.p, s);
       if (e == hipSuccess) e = kd_build(elems.p, n, m->nodes.p, s);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -487,6 +512,19 @@ int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_phot
   }
   *out = m;
   return PM_OK;
+}
+
+int pm_photon_map_create(const pm_photon* a, int64_t na, float pa, const pm_photon* b, int64_t nb, float pb,
+                         pm_photon_map** out, void* stream) {
+  if (!out || na < 0 || nb < 0 || (na > 0 && !a) || (nb > 0 && !b)) return PM_ERR_INVALID;
+  return map_create_runs(runs_of(a, na, pa, b, nb, pb), out, stream);
+}
+
+int pm_photon_map_create_rows(const pm_photon_rows* a, float pa, const pm_photon_rows* b, float pb,
+                              pm_photon_map** out, void* stream) {
+  RowRuns runs;
+  if (!out || !runs_of_rows(a, pa, runs) || !runs_of_rows(b, pb, runs)) return PM_ERR_INVALID;
+  return map_create_runs(runs, out, stream);
 }
 
 int pm_photon_map_size(const pm_photon_map* m, int64_t* n) {
@@ -527,18 +565,15 @@ struct pm_kd_shard_plan {
   int device = 0;
 };
 
-int pm_kd_shard_plan_create(const pm_photon* a, int64_t na, float pa, const pm_photon* b, int64_t nb, float pb,
-                            int32_t world, pm_kd_shard_plan** out, void* stream) {
-  if (!out || na < 0 || nb < 0 || world < 1 || (na > 0 && !a) || (nb > 0 && !b)) return PM_ERR_INVALID;
+static int plan_create_runs(const RowRuns& runs, int32_t world, pm_kd_shard_plan** out, void* stream) {
   *out = nullptr;
-  const int64_t n = na + nb;
+  const int64_t n = rows_total(runs);
   if (n >= kMaxMapPhotons) return PM_ERR_INVALID;
   int st = require_device();
   if (st != PM_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
-  PM_PTR_DEVICE(alloc_scope, a);
-  PM_PTR_DEVICE(alloc_scope, b);
+  if (runs_elsewhere(runs, alloc_scope.dev)) return PM_ERR_DEVICE;
   pm_kd_shard_plan* p = new pm_kd_shard_plan;
   p->made_on = s;
   p->device = alloc_scope.dev;
@@ -553,7 +588,7 @@ int pm_kd_shard_plan_create(const pm_photon* a, int64_t na, float pa, const pm_p
     }
     reset_phase(PH_KDBUILD);
     PhaseTimer tm(PH_KDBUILD, s);
-    e = launch_elems_from_photons(a, na, b, nb, pa, pb, p->elems.p, p->payload.p, s);
+    e = launch_elems_from_rows(runs, p->elems.p, p->payload.p, s);
     const int L = shard_levels(world);
     if (e == hipSuccess && world > 1 && shard_ok(n, L)) {
       p->top.alloc((size_t)1 << L);
@@ -573,6 +608,19 @@ int pm_kd_shard_plan_create(const pm_photon* a, int64_t na, float pa, const pm_p
   }
   *out = p;
   return PM_OK;
+}
+
+int pm_kd_shard_plan_create(const pm_photon* a, int64_t na, float pa, const pm_photon* b, int64_t nb, float pb,
+                            int32_t world, pm_kd_shard_plan** out, void* stream) {
+  if (!out || na < 0 || nb < 0 || world < 1 || (na > 0 && !a) || (nb > 0 && !b)) return PM_ERR_INVALID;
+  return plan_create_runs(runs_of(a, na, pa, b, nb, pb), world, out, stream);
+}
+
+int pm_kd_shard_plan_create_rows(const pm_photon_rows* a, float pa, const pm_photon_rows* b, float pb, int32_t world,
+                                 pm_kd_shard_plan** out, void* stream) {
+  RowRuns runs;
+  if (!out || world < 1 || !runs_of_rows(a, pa, runs) || !runs_of_rows(b, pb, runs)) return PM_ERR_INVALID;
+  return plan_create_runs(runs, world, out, stream);
 }
 
 int pm_kd_shard_subtrees(const pm_kd_shard_plan* p, int32_t* count, int64_t* sizes) {
@@ -719,11 +767,9 @@ int pm_kd_top_sel_step(pm_kd_top_sel* h, int64_t* d_buf, int64_t* count, int32_t
   return map_err(e);
 }
 
-int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* h, const pm_photon* a, int64_t na, float pa,
-                                     const pm_photon* b, int64_t nb, float pb, pm_kd_shard_plan** out,
-                                     void* stream) {
-  if (!h || !out || na < 0 || nb < 0 || (na > 0 && !a) || (nb > 0 && !b) || na + nb != h->n_total ||
-      (h->split && h->sel.level < h->sel.L))
+static int plan_from_sel_runs(const pm_kd_top_sel* h, const RowRuns& runs, pm_kd_shard_plan** out, void* stream) {
+  const int64_t n = rows_total(runs);
+  if (n != h->n_total || (h->split && h->sel.level < h->sel.L))
     return PM_ERR_INVALID;   // the gathered map, after the last step
   *out = nullptr;
   int st = require_device();
@@ -731,9 +777,7 @@ int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* h, const pm_photon* a,
   hipStream_t s = (hipStream_t)stream;
   AllocStream alloc_scope(s);
   PM_SAME_DEVICE(alloc_scope, h);
-  PM_PTR_DEVICE(alloc_scope, a);
-  PM_PTR_DEVICE(alloc_scope, b);
-  const int64_t n = na + nb;
+  if (runs_elsewhere(runs, alloc_scope.dev)) return PM_ERR_DEVICE;
   pm_kd_shard_plan* p = new pm_kd_shard_plan;
   p->made_on = s;
   p->device = alloc_scope.dev;
@@ -749,7 +793,7 @@ int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* h, const pm_photon* a,
     reset_phase(PH_KDBUILD);
     PhaseTimer tm(PH_KDBUILD, s);
     if (!h->split) {
-      e = launch_elems_from_photons(a, na, b, nb, pa, pb, p->elems.p, p->payload.p, s);
+      e = launch_elems_from_rows(runs, p->elems.p, p->payload.p, s);
     } else {
       // elements, payload and subtrees in one pass over the gathered photons
       // (the selection's top nodes hold the split coordinates), then the top
@@ -758,8 +802,7 @@ int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* h, const pm_photon* a,
       p->top.alloc((size_t)1 << L);
       p->sub.alloc(n);
       if (!p->top.p || !p->sub.p) e = hipErrorOutOfMemory;
-      if (e == hipSuccess)
-        e = kd_shard_elems_classify(a, na, b, nb, pa, pb, h->sel.top.p, L, p->elems.p, p->payload.p, p->sub.p, s);
+      if (e == hipSuccess) e = kd_shard_elems_classify(runs, h->sel.top.p, L, p->elems.p, p->payload.p, p->sub.p, s);
       if (e == hipSuccess)
         e = hipMemcpyAsync(p->top.p, h->sel.top.p, sizeof(float4) * (((size_t)1 << L) - 1), hipMemcpyDeviceToDevice,
                            s);
@@ -777,6 +820,20 @@ int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* h, const pm_photon* a,
   }
   *out = p;
   return PM_OK;
+}
+
+int pm_kd_shard_plan_create_from_sel(const pm_kd_top_sel* h, const pm_photon* a, int64_t na, float pa,
+                                     const pm_photon* b, int64_t nb, float pb, pm_kd_shard_plan** out,
+                                     void* stream) {
+  if (!h || !out || na < 0 || nb < 0 || (na > 0 && !a) || (nb > 0 && !b)) return PM_ERR_INVALID;
+  return plan_from_sel_runs(h, runs_of(a, na, pa, b, nb, pb), out, stream);
+}
+
+int pm_kd_shard_plan_create_from_sel_rows(const pm_kd_top_sel* h, const pm_photon_rows* a, float pa,
+                                          const pm_photon_rows* b, float pb, pm_kd_shard_plan** out, void* stream) {
+  RowRuns runs;
+  if (!h || !out || !runs_of_rows(a, pa, runs) || !runs_of_rows(b, pb, runs)) return PM_ERR_INVALID;
+  return plan_from_sel_runs(h, runs, out, stream);
 }
 
 int pm_kd_top_sel_destroy(pm_kd_top_sel* h) {

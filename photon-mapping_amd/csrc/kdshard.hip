@@ -687,30 +687,37 @@ hipError_t KdTopSel::step(int64_t* red, int64_t* count, int* op, hipStream_t s) 
   return issue(red, count, op, s);
 }
 
-// The gathered photons -> elements + payload (k_elems_from_photons) and each
-// element's subtree (k_shard_sub) in one pass: the selection's top nodes
-// carry the split coordinates top_path reads.
-__global__ void k_shard_elems_classify(const pm_photon* __restrict__ a, int64_t na, const pm_photon* __restrict__ b,
-                                       int64_t nb, float pa, float pb, const float4* __restrict__ top, int L,
+// The gathered photons -> elements + payload (k_elems_from_rows) and each
+// element's subtree (k_shard_sub) in one pass per run of rows: the selection's
+// top nodes carry the split coordinates top_path reads.
+__global__ void k_shard_elems_classify(const float* __restrict__ rows, int stride, int coff, int64_t n, int64_t id0,
+                                       float power, const float4* __restrict__ top, int L,
                                        float4* __restrict__ elems, float4* __restrict__ payload,
                                        uint8_t* __restrict__ sub) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= na + nb) return;
-  const pm_photon p = i < na ? a[i] : b[i - na];
-  const float4 e = make_float4(shard_kd_coord(p.pos.x), shard_kd_coord(p.pos.y), shard_kd_coord(p.pos.z),
-                               __int_as_float((int)i));
-  elems[i] = e;
-  payload[i] = make_float4(p.color.x, p.color.y, p.color.z, i < na ? pa : pb);
+  if (i >= n) return;
+  const float* r = rows + i * stride;
+  const int64_t id = id0 + i;
+  const float4 e = make_float4(shard_kd_coord(r[0]), shard_kd_coord(r[1]), shard_kd_coord(r[2]),
+                               __int_as_float((int)id));
+  elems[id] = e;
+  payload[id] = make_float4(r[coff], r[coff + 1], r[coff + 2], power);
   const int j = top_path(e, top, L);
-  sub[i] = j < 0 ? 255 : (uint8_t)j;
+  sub[id] = j < 0 ? 255 : (uint8_t)j;
 }
 
-hipError_t kd_shard_elems_classify(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
-                                   float pb, const float4* top, int L, float4* elems, float4* payload, uint8_t* sub,
-                                   hipStream_t s) {
-  if (na + nb <= 0) return hipSuccess;
-  k_shard_elems_classify<<<grid_for(na + nb, 256), 256, 0, s>>>(a, na, b, nb, pa, pb, top, L, elems, payload, sub);
-  return hipGetLastError();
+hipError_t kd_shard_elems_classify(const RowRuns& runs, const float4* top, int L, float4* elems, float4* payload,
+                                   uint8_t* sub, hipStream_t s) {
+  int64_t id0 = 0;
+  for (const RowRun& r : runs) {
+    if (r.n > 0) {
+      k_shard_elems_classify<<<grid_for(r.n, 256), 256, 0, s>>>(r.rows, r.stride, r.coff, r.n, id0, r.power, top, L,
+                                                               elems, payload, sub);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    id0 += r.n;
+  }
+  return hipSuccess;
 }
 
 hipError_t kd_shard_top_fix(const float4* elems, float4* top, int L, hipStream_t s) {

@@ -1971,13 +1971,14 @@ static hipError_t kd_build_lists(const float4* elems, int64_t n, float4* nodes, 
 // gather radius.
 __device__ __forceinline__ float kd_coord(float x) { return x != x ? __int_as_float(0x7f800000) : x; }
 
-__global__ void k_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
-                                     float pb, float4* elems, float4* payload) {
+// one run of photon rows -> elements [id0, id0 + n) and their payload
+__global__ void k_elems_from_rows(const float* __restrict__ rows, int stride, int coff, int64_t n, int64_t id0,
+                                  float power, float4* __restrict__ elems, float4* __restrict__ payload) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= na + nb) return;
-  const pm_photon p = i < na ? a[i] : b[i - na];
-  elems[i] = make_float4(kd_coord(p.pos.x), kd_coord(p.pos.y), kd_coord(p.pos.z), __int_as_float((int)i));
-  payload[i] = make_float4(p.color.x, p.color.y, p.color.z, i < na ? pa : pb);
+  if (i >= n) return;
+  const float* r = rows + i * stride;
+  elems[id0 + i] = make_float4(kd_coord(r[0]), kd_coord(r[1]), kd_coord(r[2]), __int_as_float((int)(id0 + i)));
+  payload[id0 + i] = make_float4(r[coff], r[coff + 1], r[coff + 2], power);
 }
 
 __global__ void k_elems_from_kd(const pm_kd_photon* in, int64_t n, float4* elems) {
@@ -2051,11 +2052,23 @@ __global__ void k_bounds_final(const unsigned* ob, pm_box* box) {
   box->upper = {v[3], v[4], v[5]};
 }
 
-hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
-                                     float pb, float4* elems, float4* payload, hipStream_t s) {
-  if (na + nb <= 0) return hipSuccess;
-  k_elems_from_photons<<<grid_for(na + nb, 256), 256, 0, s>>>(a, na, b, nb, pa, pb, elems, payload);
-  return hipGetLastError();
+int64_t rows_total(const RowRuns& runs) {
+  int64_t n = 0;
+  for (const RowRun& r : runs) n += r.n;
+  return n;
+}
+
+hipError_t launch_elems_from_rows(const RowRuns& runs, float4* elems, float4* payload, hipStream_t s) {
+  int64_t id0 = 0;
+  for (const RowRun& r : runs) {
+    if (r.n > 0) {
+      k_elems_from_rows<<<grid_for(r.n, 256), 256, 0, s>>>(r.rows, r.stride, r.coff, r.n, id0, r.power, elems,
+                                                          payload);
+      PM_HIP_TRY(hipGetLastError());
+    }
+    id0 += r.n;
+  }
+  return hipSuccess;
 }
 
 hipError_t kd_build_records(pm_kd_photon* d, int64_t n, pm_box* bounds, hipStream_t s) {

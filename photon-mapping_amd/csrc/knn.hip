@@ -842,10 +842,25 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
   return hipStreamSynchronize(s);   // the pass bounds are freed on return
 }
 
+// A/B knob (variant libraries only): run the k = 50 gather through the
+// collect-and-sort kernel (rows of 64 * PM_GATHER50_WIDE keys) instead of the
+// VGPR list walk
+#ifndef PM_GATHER50_WIDE
+#define PM_GATHER50_WIDE 0
+#endif
+template <int S>
+static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out,
+                                       hipStream_t s, int k, const uint32_t* perm);
+
 hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,
                          int tag, const uint32_t* perm) {
   if (nq <= 0) return hipSuccess;
   const int n = (int)m->n;
+#if PM_GATHER50_WIDE && !PM_CHECK_VARIANT
+  (void)tag;
+  (void)n;
+  return launch_gather_wide_s<PM_GATHER50_WIDE>(m, qb, nq, out, s, kKNearest, perm);
+#endif
 #if PM_CHECK_VARIANT
   const int g = grid_for(nq, 256);
   if (tag == 1) k_gather_plain<1><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm);

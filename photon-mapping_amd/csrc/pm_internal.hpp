@@ -127,11 +127,23 @@ struct KdTopSel {
   hipError_t consume(const int64_t* red, hipStream_t s);
 };
 hipError_t kd_shard_top_fix(const float4* elems, float4* top, int L, hipStream_t s);
-hipError_t kd_shard_elems_classify(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
-                                   float pb, const float4* top, int L, float4* elems, float4* payload, uint8_t* sub,
-                                   hipStream_t s);
-hipError_t launch_elems_from_photons(const pm_photon* a, int64_t na, const pm_photon* b, int64_t nb, float pa,
-                                     float pb, float4* elems, float4* payload, hipStream_t s);
+// One contiguous run of photon rows (pm_photon_rows segment, or a whole
+// pm_photon array): n rows of `stride` floats, position at 0..2, colour at
+// coff..coff+2, gather power `power`. A map's photons are a list of runs,
+// concatenated in order (original index = position in the concatenation).
+struct RowRun {
+  const float* rows;
+  int stride, coff;
+  int64_t n;
+  float power;
+};
+using RowRuns = std::vector<RowRun>;
+int64_t rows_total(const RowRuns& runs);
+// elements (x, y, z, original index) + payload (colour, power), one launch per run
+hipError_t launch_elems_from_rows(const RowRuns& runs, float4* elems, float4* payload, hipStream_t s);
+// the same and each element's subtree below the top L levels (top_path), one pass
+hipError_t kd_shard_elems_classify(const RowRuns& runs, const float4* top, int L, float4* elems, float4* payload,
+                                   uint8_t* sub, hipStream_t s);
 
 // gatherPhotons over k != 50 neighbours (pm_knn passes + one summing kernel).
 hipError_t launch_gather_k(const pm_photon_map* m, const float4* d_query, int64_t nq, float4* d_out, hipStream_t s,

@@ -129,7 +129,17 @@ class Config(C.Structure):
                 ("error", C.c_char * 512)]
 
 
+ROWS_MAX_SEGS = 32   # PM_ROWS_MAX_SEGS
+
+
+class PhotonRowsStruct(C.Structure):   # pm_photon_rows
+    _fields_ = [("d_rows", C.c_void_p), ("row_floats", C.c_int32), ("color_offset", C.c_int32),
+                ("nseg", C.c_int32), ("reserved", C.c_int32), ("seg_row0", C.c_int64 * ROWS_MAX_SEGS),
+                ("seg_count", C.c_int64 * ROWS_MAX_SEGS)]
+
+
 assert C.sizeof(Material) == 28 and C.sizeof(Photon) == 40 and C.sizeof(KdPhoton) == 44
+assert C.sizeof(PhotonRowsStruct) == 24 + 16 * ROWS_MAX_SEGS
 assert C.sizeof(Light) == 64
 
 # ----------------------------------------------------------------- library
@@ -155,6 +165,7 @@ _SIGNATURES = {
                                    C.POINTER(C.c_int64), _P]),
     "pm_kdtree_build": (C.c_int, [_P, C.c_int64, _P, _P]),
     "pm_photon_map_create": (C.c_int, [_P, C.c_int64, C.c_float, _P, C.c_int64, C.c_float, C.POINTER(_P), _P]),
+    "pm_photon_map_create_rows": (C.c_int, [_P, C.c_float, _P, C.c_float, C.POINTER(_P), _P]),
     "pm_photon_map_size": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "pm_photon_map_export": (C.c_int, [_P, _P, _P]),
     "pm_photon_map_destroy": (C.c_int, [_P]),
@@ -163,12 +174,14 @@ _SIGNATURES = {
     "pm_kd_shard_subtrees": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
     "pm_kd_shard_build": (C.c_int, [_P, C.c_int32, _P, _P]),
     "pm_photon_map_create_sharded": (C.c_int, [_P, _P, C.POINTER(_P), _P]),
+    "pm_kd_shard_plan_create_rows": (C.c_int, [_P, C.c_float, _P, C.c_float, C.c_int32, C.POINTER(_P), _P]),
     "pm_kd_shard_plan_destroy": (C.c_int, [_P]),
     "pm_kd_top_sel_create": (C.c_int, [_P, C.c_int64, C.c_int64, _P, C.c_int64, C.c_int64, C.c_int64, C.c_int32,
                                        C.POINTER(_P), _P]),
     "pm_kd_top_sel_step": (C.c_int, [_P, _P, C.POINTER(C.c_int64), C.POINTER(C.c_int32), _P]),
     "pm_kd_shard_plan_create_from_sel": (C.c_int, [_P, _P, C.c_int64, C.c_float, _P, C.c_int64, C.c_float,
                                                    C.POINTER(_P), _P]),
+    "pm_kd_shard_plan_create_from_sel_rows": (C.c_int, [_P, _P, C.c_float, _P, C.c_float, C.POINTER(_P), _P]),
     "pm_kd_top_sel_destroy": (C.c_int, [_P]),
     "pm_knn": (C.c_int, [_P, _P, C.c_int64, C.c_int32, C.c_float, _P, _P, _P, _P]),
     "pm_gather": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P]),
@@ -467,15 +480,80 @@ PHOTON_POWER = 1.0                       # ray-tracer/src/hostCode.cu:21
 CAUSTICS_PHOTON_POWER = PHOTON_POWER * 0.5   # hostCode.cu:22
 
 
+class PhotonRows:
+    """One photon set as row segments of one device buffer (pm_photon_rows):
+    what the N > 1 exchange delivers -- (position, colour) rows padded per rank
+    in one all-gather buffer -- handed to the maps without a compaction or a
+    re-expansion copy. `buf` is a 2-D float32 cuda tensor (rows of
+    buf.shape[1] floats, position at 0..2, colour at color_offset..+2);
+    `segments` = [(first row, rows), ...] in map order."""
+
+    def __init__(self, buf, segments, color_offset: int):
+        assert buf.dim() == 2 and buf.dtype.is_floating_point and buf.is_contiguous()
+        assert len(segments) <= ROWS_MAX_SEGS and 3 <= color_offset <= buf.shape[1] - 3
+        assert all(0 <= r0 and 0 <= c and r0 + c <= buf.shape[0] for r0, c in segments)
+        self.buf, self.segments, self.color_offset = buf, [(int(r0), int(c)) for r0, c in segments], int(color_offset)
+        self.n = sum(c for _, c in self.segments)
+
+    @classmethod
+    def of_photons(cls, t):
+        """A pm_photon tensor (n, 10): one segment, colour at float 7."""
+        return cls(t, [(0, t.shape[0])], 7)
+
+    @classmethod
+    def of_padded(cls, buf, counts, m: int, color_offset: int = 3):
+        """The all-gather's padded buffer: rank r's counts[r] rows start at row r * m."""
+        return cls(buf, [(r * m, c) for r, c in enumerate(counts)], color_offset)
+
+    def struct(self):
+        st = PhotonRowsStruct()
+        st.d_rows = self.buf.data_ptr() if self.n else None
+        st.row_floats, st.color_offset, st.nseg = self.buf.shape[1], self.color_offset, len(self.segments)
+        for k, (r0, c) in enumerate(self.segments):
+            st.seg_row0[k], st.seg_count[k] = r0, c
+        return st
+
+    def rows(self):
+        """(n, 6) position + colour, concatenated (a copy; tests and tools)."""
+        import torch
+        parts = [self.buf[r0: r0 + c] for r0, c in self.segments]
+        cat = torch.cat(parts) if parts else self.buf[:0]
+        co = self.color_offset
+        return torch.cat([cat[:, 0:3], cat[:, co: co + 3]], dim=1).contiguous()
+
+    def photons(self):
+        """pm_photon rows (n, 10), direction and power zero (a copy; tests and tools)."""
+        import torch
+        r = self.rows()
+        t = torch.zeros((r.shape[0], 10), dtype=r.dtype, device=r.device)
+        t[:, 0:3], t[:, 7:10] = r[:, 0:3], r[:, 3:6]
+        return t
+
+
+def _rows_arg(x):
+    """None / pm_photon tensor / PhotonRows -> (pm_photon_rows struct or None, n)"""
+    if x is None:
+        return None, 0
+    r = x if isinstance(x, PhotonRows) else PhotonRows.of_photons(x)
+    return (C.byref(r.struct()) if r.n else None), r.n
+
+
 class PhotonMap:
-    """Photon kd-tree + gather payload (loadPhotons + cukd::buildTree)."""
+    """Photon kd-tree + gather payload (loadPhotons + cukd::buildTree). The sets
+    are pm_photon tensors (n, 10) or PhotonRows (pm_photon_map_create_rows)."""
 
     def __init__(self, a, power_a: float, b=None, power_b: float = 0.0, stream=None):
         h = _P()
-        na = 0 if a is None else a.shape[0]
-        nb = 0 if b is None else b.shape[0]
-        _check(_lib.pm_photon_map_create(_ptr(a) if na else None, na, float(power_a), _ptr(b) if nb else None, nb,
-                                         float(power_b), C.byref(h), _stream(stream)), "pm_photon_map_create")
+        if isinstance(a, PhotonRows) or isinstance(b, PhotonRows):
+            ra, na = _rows_arg(a)
+            rb, nb = _rows_arg(b)
+            _check(_lib.pm_photon_map_create_rows(ra, float(power_a), rb, float(power_b), C.byref(h),
+                                                  _stream(stream)), "pm_photon_map_create_rows")
+        else:
+            na = 0 if a is None else a.shape[0]
+            nb = 0 if b is None else b.shape[0]
+            _check(_lib.pm_photon_map_create(_ptr(a) if na else None, na, float(power_a), _ptr(b) if nb else None,
+                                             nb, float(power_b), C.byref(h), _stream(stream)), "pm_photon_map_create")
         self._h = h
         self.n = na + nb
 
@@ -511,18 +589,30 @@ class KdShardPlan:
     def __init__(self, a, power_a: float, b=None, power_b: float = 0.0, world: int = 1, stream=None,
                  sel: "KdTopSel" = None):
         """sel: a finished KdTopSel (the distributed top selection) instead of
-        selecting the top levels here from the gathered photons."""
+        selecting the top levels here from the gathered photons. The sets are
+        pm_photon tensors or PhotonRows (the exchange's buffer as it is)."""
         h = _P()
-        na = 0 if a is None else a.shape[0]
-        nb = 0 if b is None else b.shape[0]
-        if sel is None:
-            _check(_lib.pm_kd_shard_plan_create(_ptr(a) if na else None, na, float(power_a),
-                                                _ptr(b) if nb else None, nb, float(power_b), int(world), C.byref(h),
-                                                _stream(stream)), "pm_kd_shard_plan_create")
+        if isinstance(a, PhotonRows) or isinstance(b, PhotonRows):
+            ra, na = _rows_arg(a)
+            rb, nb = _rows_arg(b)
+            if sel is None:
+                _check(_lib.pm_kd_shard_plan_create_rows(ra, float(power_a), rb, float(power_b), int(world),
+                                                         C.byref(h), _stream(stream)), "pm_kd_shard_plan_create_rows")
+            else:
+                _check(_lib.pm_kd_shard_plan_create_from_sel_rows(sel._h, ra, float(power_a), rb, float(power_b),
+                                                                  C.byref(h), _stream(stream)),
+                       "pm_kd_shard_plan_create_from_sel_rows")
         else:
-            _check(_lib.pm_kd_shard_plan_create_from_sel(sel._h, _ptr(a) if na else None, na, float(power_a),
-                                                         _ptr(b) if nb else None, nb, float(power_b), C.byref(h),
-                                                         _stream(stream)), "pm_kd_shard_plan_create_from_sel")
+            na = 0 if a is None else a.shape[0]
+            nb = 0 if b is None else b.shape[0]
+            if sel is None:
+                _check(_lib.pm_kd_shard_plan_create(_ptr(a) if na else None, na, float(power_a),
+                                                    _ptr(b) if nb else None, nb, float(power_b), int(world),
+                                                    C.byref(h), _stream(stream)), "pm_kd_shard_plan_create")
+            else:
+                _check(_lib.pm_kd_shard_plan_create_from_sel(sel._h, _ptr(a) if na else None, na, float(power_a),
+                                                             _ptr(b) if nb else None, nb, float(power_b), C.byref(h),
+                                                             _stream(stream)), "pm_kd_shard_plan_create_from_sel")
         self._h = h
         self.n = na + nb
         cnt = C.c_int32(0)

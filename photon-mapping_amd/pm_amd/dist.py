@@ -72,33 +72,51 @@ def shard_range(total: int, rank: int, world: int):
 
 class _Gathered:
     """An all-gather in flight (allgather_rows_start); wait() returns the rows
-    concatenated in rank order."""
+    concatenated in rank order (a copy), rows() the padded buffer itself as
+    PhotonRows (device tensors: no copy; rank r at rows [r m, r m + n_r))."""
 
     def __init__(self, work, out, ns, m, world, parts=None):
         self.work, self.out, self.ns, self.m, self.world, self.parts = work, out, ns, m, world, parts
 
-    def wait(self):
-        import torch
+    def _done(self):
         if self.work is not None:
             self.work.wait()
+            self.work = None
+
+    def wait(self):
+        import torch
+        self._done()
         if self.parts is None:
             self.parts = [self.out[r * self.m: r * self.m + self.ns[r]] for r in range(self.world)]
         return torch.cat(self.parts)
 
+    def rows(self):
+        from pm_amd import PhotonRows
+        self._done()
+        return PhotonRows.of_padded(self.out, self.ns, self.m, color_offset=3)
 
-def allgather_rows_start(t, world: int, dist):
+
+def allgather_rows_start(t, world: int, dist, pack=None):
     """Variable-length all-gather of an (n_r, C) tensor: the counts are exchanged
     first (the host sizes the padded buffer), then ONE padded all-gather is
     started asynchronously on device tensors (RCCL runs it on its own stream, so
-    the caller can overlap work on the current stream until wait())."""
+    the caller can overlap work on the current stream until wait()).
+    pack(t, out): writes t's C-column rows into `out` (the padded buffer's first
+    n_r rows) instead of a copy of t itself (pm_photon -> position + colour in
+    one pass)."""
     import torch
     n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
     ns = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(ns, n)
     ns = [int(x.item()) for x in ns]
     m = max(1, max(ns))
-    pad = torch.zeros((m, t.shape[1]), dtype=t.dtype, device=t.device)
-    pad[: t.shape[0]] = t
+    cols = t.shape[1] if pack is None else PACKED_COLS
+    pad = torch.empty((m, cols), dtype=t.dtype, device=t.device)
+    pad[t.shape[0]:].zero_()
+    if pack is None:
+        pad[: t.shape[0]] = t
+    else:
+        pack(t, pad[: t.shape[0]])
     if t.device.type == "cuda":
         out = torch.empty((world * m, t.shape[1]), dtype=t.dtype, device=t.device)
         work = dist.all_gather_into_tensor(out, pad, async_op=True)
@@ -176,10 +194,16 @@ class HostStagedDist:
         self.d.destroy_process_group()
 
 
-def pack_rows(t):
-    """pm_photon rows (n, 10) -> (n, 6): position, colour."""
+PACKED_COLS = 6   # position + colour: what a map reads of a photon
+
+
+def pack_rows(t, out=None):
+    """pm_photon rows (n, 10) -> (n, 6): position, colour (into `out` if given)."""
     import torch
-    return torch.cat([t[:, 0:3], t[:, 7:10]], dim=1).contiguous()
+    if out is None:
+        return torch.cat([t[:, 0:3], t[:, 7:10]], dim=1).contiguous()
+    torch.cat([t[:, 0:3], t[:, 7:10]], dim=1, out=out)
+    return out
 
 
 def unpack_rows(p):
@@ -321,11 +345,18 @@ def _pm():
 class GpuBackend:
     """libpm_hip.so through pm_amd (device tensors on the current cuda device)."""
 
-    def __init__(self, scene, lights, cfg: FrameConfig, rank: int, world: int, gbuf=None, cbuf=None):
+    def __init__(self, scene, lights, cfg: FrameConfig, rank: int, world: int, gbuf=None, cbuf=None,
+                 sel_group=None):
+        """sel_group: the communicator of the distributed top selection's small
+        all-reduces (N > 1, cfg.dist_top). Create it right after
+        init_process_group (`dist.new_group()`), outside any frame: created
+        lazily, its RCCL communicator would be set up while the photon
+        all-gather is in flight on the default group."""
         import pm_amd
         self.pm = pm_amd
         self.scene, self.lights, self.cfg = scene, lights, cfg
         self.gbuf, self.cbuf = gbuf, cbuf
+        self._sel_group = sel_group
         self.cam = pm_amd.setup_camera(cfg.camera["look_from"], cfg.camera["look_at"], cfg.camera["look_up"],
                                        cfg.camera["fovy"], cfg.width, cfg.height)
         self.phase = {}
@@ -518,9 +549,22 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
         rgba = backend.render(gm, cm, rank, world, rgba)
     if world > 1:
         dist.reduce(rgba, dst=0, op=dist.ReduceOp.SUM)
-    info = {"n_global": int(gm.n), "n_caustic": int(cm.n), "n_global_rows": int(g.shape[0]),
+    info = {"n_global": int(gm.n), "n_caustic": int(cm.n), "n_global_rows": nrows(g),
             "us": dict(backend.phase)}
     return rgba, info
+
+
+def _gathered_set(x):
+    """A finished photon all-gather as a map input: PhotonRows over the padded
+    device buffer, or (host tensors: the CPU test backends) pm_photon rows."""
+    if x.out is not None:
+        return x.rows()
+    return unpack_rows(x.wait())
+
+
+def nrows(x) -> int:
+    """photons in a set (tensor rows or PhotonRows)"""
+    return int(x.n if hasattr(x, "segments") else x.shape[0])
 
 
 def _maps(backend, rank: int, world: int, dist, pending=None, early_caustic: bool = False):
@@ -537,16 +581,19 @@ def _maps(backend, rank: int, world: int, dist, pending=None, early_caustic: boo
     sel = None
     if world > 1:
         # only position and colour reach the maps (kd nodes + gather payload):
-        # 24 of the 40 bytes of a photon cross xGMI
+        # 24 of the 40 bytes of a photon cross xGMI, packed straight into the
+        # padded all-gather buffer; on the device the maps read that buffer as
+        # it is (PhotonRows: rank r's rows at [r m, r m + n_r)), with no
+        # compaction and no re-expansion to pm_photon rows
         clock = _PhaseClock(g.device.type == "cuda")
         g_local, c_local = g, c
-        cx = allgather_rows_start(pack_rows(c_local), world, dist)
-        c = unpack_rows(cx.wait())
-        xfer = allgather_rows_start(pack_rows(g_local), world, dist)
+        cx = allgather_rows_start(c_local, world, dist, pack=pack_rows)
+        c = _gathered_set(cx)
+        xfer = allgather_rows_start(g_local, world, dist, pack=pack_rows)
         cm = backend.caustic_map(c)   # overlaps the global photons' transfer
         if hasattr(backend, "top_selection"):   # so does the top selection (own photons only)
             sel = backend.top_selection(g_local, c_local, xfer.ns, cx.ns, rank, world, dist)
-        g = unpack_rows(xfer.wait())
+        g = _gathered_set(xfer)
         backend.phase["exchange"] = clock.stop_us()
     else:
         backend.phase["exchange"] = 0.0

@@ -36,11 +36,13 @@ def test_struct_sizes_match_header():
     import pm_amd
     src = r"""
 #include <stdio.h>
+#include <stddef.h>
 #include "pm.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(pm_material), sizeof(pm_mesh), sizeof(pm_light),
-         sizeof(pm_photon), sizeof(pm_kd_photon), sizeof(pm_ray), sizeof(pm_hit), sizeof(pm_trace_params),
-         sizeof(pm_render_params), sizeof(pm_config));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(pm_material), sizeof(pm_mesh),
+         sizeof(pm_light), sizeof(pm_photon), sizeof(pm_kd_photon), sizeof(pm_ray), sizeof(pm_hit),
+         sizeof(pm_trace_params), sizeof(pm_render_params), sizeof(pm_config), sizeof(pm_photon_rows),
+         offsetof(pm_photon_rows, seg_count));
   return 0;
 }
 """
@@ -52,7 +54,8 @@ int main(void) {
                    check=True)
     got = list(map(int, subprocess.run([os.path.join(d, "s")], capture_output=True, text=True).stdout.split()))
     exp = [C.sizeof(t) for t in (pm_amd.Material, pm_amd.Mesh, pm_amd.Light, pm_amd.Photon, pm_amd.KdPhoton,
-                                 pm_amd.Ray, pm_amd.Hit, pm_amd.TraceParams, pm_amd.RenderParams, pm_amd.Config)]
+                                 pm_amd.Ray, pm_amd.Hit, pm_amd.TraceParams, pm_amd.RenderParams, pm_amd.Config,
+                                 pm_amd.PhotonRowsStruct)] + [pm_amd.PhotonRowsStruct.seg_count.offset]
     assert got == exp
     assert got[:5] == [28, got[1], 64, 40, 44]      # reference record sizes
 
@@ -61,8 +64,9 @@ def test_status_strings():
     import pm_amd
     for s in range(9):
         assert pm_amd.lib.pm_status_string(s) != b"unknown status"
-    # 2: pm_render_params.caustic_k; 3: PM_ERR_DEVICE, pm_device_pool_stats; 4: pm_kd_top_sel_*
-    assert pm_amd.lib.pm_abi_version() == 4
+    # 2: pm_render_params.caustic_k; 3: PM_ERR_DEVICE, pm_device_pool_stats; 4: pm_kd_top_sel_*;
+    # 5: pm_photon_rows (pm_photon_map_create_rows, pm_kd_shard_plan_create_rows / _from_sel_rows)
+    assert pm_amd.lib.pm_abi_version() == 5
 
 
 def test_no_cpu_fallback_without_gpu(cornell):

@@ -15,10 +15,15 @@ def _copy_tree(dst):
     os.makedirs(os.path.join(dst, "include"))
     shutil.copy(os.path.join(ROOT, "photon-mapping_amd", "Makefile"), os.path.join(dst, "photon-mapping_amd"))
     shutil.copy(os.path.join(ROOT, "include", "pm.h"), os.path.join(dst, "include"))
+    flags = os.path.join(ROOT, "photon-mapping_amd", "lib", "build_flags.txt")
+    if os.path.exists(flags):
+        os.makedirs(os.path.join(dst, "photon-mapping_amd", "lib"))
+        shutil.copy(flags, os.path.join(dst, "photon-mapping_amd", "lib"))
 
 
 def test_source_digest_tracks_the_sources(tmp_path, monkeypatch):
     import bench
+    monkeypatch.delenv("PM_HIP_LIB", raising=False)
     d0 = bench.source_digest()
     assert len(d0) == 64 and d0 == bench.source_digest()
     _copy_tree(str(tmp_path))
@@ -31,3 +36,24 @@ def test_source_digest_tracks_the_sources(tmp_path, monkeypatch):
     d1 = bench.source_digest()
     (tmp_path / "photon-mapping_amd" / "csrc" / "notes.txt").write_text("y")
     assert bench.source_digest() == d1            # non-source files do not count
+
+
+def test_source_digest_tracks_the_build_flags(tmp_path, monkeypatch):
+    """a variant library (same sources, other -D flags) is not the
+    library the counters were collected on"""
+    import bench
+    monkeypatch.delenv("PM_HIP_LIB", raising=False)
+    _copy_tree(str(tmp_path))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    lib = tmp_path / "photon-mapping_amd" / "lib"
+    lib.mkdir(exist_ok=True)
+    (lib / "build_flags.txt").write_text("--offload-arch=gfx950 -O3\n")
+    d0 = bench.source_digest()
+    (lib / "build_flags.txt").write_text("--offload-arch=gfx950 -O3 -DPM_GATHER50_WIDE=2\n")
+    d1 = bench.source_digest()
+    assert d1 != d0
+    var = tmp_path / "photon-mapping_amd" / "lib_v"
+    var.mkdir()
+    (var / "build_flags.txt").write_text("--offload-arch=gfx950 -O3\n")
+    monkeypatch.setenv("PM_HIP_LIB", str(var / "libpm_hip.so"))
+    assert bench.source_digest() == d0   # the library in use decides

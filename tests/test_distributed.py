@@ -123,7 +123,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_frame_matches_single_process(world):
     import torch.multiprocessing as mp
     import pm_amd

@@ -673,3 +673,46 @@ def test_shard_plan_from_mismatched_selection_is_refused():
     with pytest.raises(pm_amd.PMError) as e:
         pmdist.shard_local(plan, 0, 4)
     assert e.value.status == pm_amd.PM_ERR_INVALID
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_photon_rows_maps_equal_photon_maps(world):
+    """pm_photon_rows (ABI 5): the maps and the sharded plan
+    built straight from the exchange's padded (position, colour) buffer -- rank
+    r's rows at [r m, r m + n_r), padding rows between -- equal those built
+    from the concatenated pm_photon arrays, bit for bit (tree, payload, and the
+    sharded build with and without the distributed top selection)."""
+    import pm_amd
+    from pm_amd import dist as pmdist
+    g, c = _synthetic_photons(70001, 5, grid=2.5), _synthetic_photons(4999, 6, grid=2.5)
+
+    def padded(t):
+        parts = [t[pmdist.shard_range(t.shape[0], r, world)[0]: pmdist.shard_range(t.shape[0], r, world)[1]]
+                 for r in range(world)]
+        ns = [p.shape[0] for p in parts]
+        m = max(ns) + 3   # extra padding rows: never read
+        buf = torch.full((world * m, 6), float("nan"), device="cuda")
+        for r, p in enumerate(parts):
+            pmdist.pack_rows(p, buf[r * m: r * m + ns[r]])
+        return pm_amd.PhotonRows.of_padded(buf, ns, m)
+
+    gr, cr = padded(g), padded(c)
+    assert gr.n == g.shape[0] and torch.equal(gr.photons()[:, [0, 1, 2, 7, 8, 9]], g[:, [0, 1, 2, 7, 8, 9]])
+    ref = pm_amd.PhotonMap(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER)
+    m = pm_amd.PhotonMap(gr, pm_amd.PHOTON_POWER, cr, pm_amd.CAUSTICS_PHOTON_POWER)
+    assert m.n == ref.n and torch.equal(m.export().view(torch.int32), ref.export().view(torch.int32))
+    mc = pm_amd.PhotonMap(cr, pm_amd.CAUSTICS_PHOTON_POWER)
+    assert torch.equal(mc.export().view(torch.int32),
+                       pm_amd.PhotonMap(c, pm_amd.CAUSTICS_PHOTON_POWER).export().view(torch.int32))
+    w = max(world, 2)
+    for sel in (None, pmdist.simulated_top_selection(pm_amd, g, c, w)[0]):
+        plan = pm_amd.KdShardPlan(gr, pm_amd.PHOTON_POWER, cr, pm_amd.CAUSTICS_PHOTON_POWER, world=w, sel=sel)
+        assert plan.n == ref.n and len(plan.sizes) > 0
+        sm = pmdist.shard_assemble(plan, torch.cat([pmdist.shard_local(plan, r, w)[0] for r in range(w)]), w)
+        assert torch.equal(sm.export().view(torch.int32), ref.export().view(torch.int32))
+    # a malformed descriptor is refused
+    bad = pm_amd.PhotonRows.of_padded(gr.buf, [1], 1)
+    bad.color_offset = 4   # colour would run past the 6-float row
+    with pytest.raises(pm_amd.PMError) as e:
+        pm_amd.PhotonMap(bad, 1.0)
+    assert e.value.status == pm_amd.PM_ERR_INVALID

@@ -33,7 +33,28 @@ if os.environ.get("SHARD", "1") == "1":
         n = base * k
         g = torch.rand((n, 10), device="cuda", dtype=torch.float32) * 100.0
         c = torch.empty((0, 10), device="cuda", dtype=torch.float32)
+        # the exchange's output: rank r's (position, colour) rows at [r m, r m + n_r)
+        # of one padded buffer (pm_amd.dist.allgather_rows_start); ROWS=1 hands it to
+        # the plan as it is (PhotonRows), ROWS=0 measures round 3's compaction +
+        # re-expansion to pm_photon rows first
+        ns = [pmdist.shard_range(n, r, world)[1] - pmdist.shard_range(n, r, world)[0] for r in range(world)]
+        mpad = max(ns)
+        gbuf = torch.zeros((world * mpad, 6), device="cuda", dtype=torch.float32)
+        for r in range(world):
+            a0, a1 = pmdist.shard_range(n, r, world)
+            pmdist.pack_rows(g[a0:a1], gbuf[r * mpad: r * mpad + ns[r]])
+        rows_mode = os.environ.get("ROWS", "1") == "1"
         for rep in range(2):
+            torch.cuda.synchronize()
+            tc = time.time()
+            if rows_mode:
+                gin = pm_amd.PhotonRows.of_padded(gbuf, ns, mpad)
+            else:
+                gin = pmdist.unpack_rows(torch.cat([gbuf[r * mpad: r * mpad + ns[r]] for r in range(world)]))
+            torch.cuda.synchronize()
+            t_copy = (time.time() - tc) * 1e3
+            print(f"  post-gather copies ({'PhotonRows: none' if rows_mode else 'cat + unpack'}): {t_copy:.1f} ms",
+                  flush=True)
             torch.cuda.synchronize()
             t0 = time.time()
             if os.environ.get("DIST", "1") == "1":
@@ -43,7 +64,7 @@ if os.environ.get("SHARD", "1") == "1":
                 sel, us = pmdist.simulated_top_selection(pm_amd, g, c, world)
                 torch.cuda.synchronize()
                 t1 = time.time()
-                plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world,
+                plan = pm_amd.KdShardPlan(gin, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world,
                                           sel=sel)
                 torch.cuda.synchronize()
                 t_from = (time.time() - t1) * 1e3
@@ -51,7 +72,7 @@ if os.environ.get("SHARD", "1") == "1":
                 print(f"  dist top selection: per-rank passes max {max(us) / 1e3:.1f} ms ({sel.steps} steps, "
                       f"{sel.steps - 1} all-reduces), plan from gathered photons {t_from:.1f} ms", flush=True)
             else:
-                plan = pm_amd.KdShardPlan(g, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world)
+                plan = pm_amd.KdShardPlan(gin, pm_amd.PHOTON_POWER, c, pm_amd.CAUSTICS_PHOTON_POWER, world=world)
                 t_plan = pm_amd.phase_us("kdbuild") / 1e3
             bufs, t_sub = [], []
             for r in range(world):
@@ -65,6 +86,6 @@ if os.environ.get("SHARD", "1") == "1":
             print(f"N={n} world={world} plan {t_plan:.1f} ms, subtree max {max(t_sub):.1f} ms, place {t_asm:.1f} ms"
                   f" -> per-rank {t_plan + max(t_sub) + t_asm:.1f} ms (+ all-gather of {everyone.numel() * 4 / 1e9:.2f} GB)",
                   flush=True)
-            del plan, bufs, everyone, m
-        del g
+            del plan, bufs, everyone, m, gin
+        del g, gbuf
         torch.cuda.empty_cache()
