@@ -611,6 +611,16 @@ constexpr int kBoxAfter = PM_BOX_AFTER;
 __device__ unsigned long long g_knn_stats[2][3][4];
 #endif
 
+#ifndef PM_GATHER_XCD
+#define PM_GATHER_XCD 0
+#endif
+// bijective blockIdx remap: blocks b with equal b % 8 (one XCD, as the
+// dispatcher deals them) get consecutive logical ids (cdna_hip_programming T1)
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nwg) {
+  const uint32_t q = nwg / 8, r = nwg % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 __device__ __forceinline__ double seed_bound(float4 lead, v3 q) {
   if (!(lead.w >= 0.f)) return 1e300;
   const double dx = (double)q.x - lead.x, dy = (double)q.y - lead.y, dz = (double)q.z - lead.z;
@@ -698,15 +708,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
   // (one lane per leader) re-walk the leaders that ran out of budget, with the
   // leaders' own cut-off; the walk and the epilogue are shared
   const int64_t nrb = (!LEADERS && nretry) ? (int64_t)retry_blocks : 0;
-  const bool redo_lane = (int64_t)blockIdx.x < nrb;
+  // XCD-aware block order (PM_GATHER_XCD): the blocks that share an XCD (b % 8)
+  // take one contiguous eighth of the walk order, so each XCD's L2 holds the
+  // tree neighbourhood of one compact query region instead of all eight
+  const uint32_t bid = PM_GATHER_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const bool redo_lane = (int64_t)bid < nrb;
   int64_t r;
   bool valid;
   if (redo_lane) {
-    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t e = bid * 256u + threadIdx.x;
     valid = e < *nretry;
     r = valid ? (int64_t)retry[e] : 0;
   } else {
-    const int64_t t = ((int64_t)blockIdx.x - nrb) * blockDim.x + threadIdx.x;
+    const int64_t t = ((int64_t)bid - nrb) * blockDim.x + threadIdx.x;
     r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
     valid = r < nq;
   }
@@ -842,25 +856,10 @@ hipError_t launch_knn(const pm_photon_map* m, const pm_float3* q, int64_t nq, in
   return hipStreamSynchronize(s);   // the pass bounds are freed on return
 }
 
-// A/B knob (variant libraries only): run the k = 50 gather through the
-// collect-and-sort kernel (rows of 64 * PM_GATHER50_WIDE keys) instead of the
-// VGPR list walk
-#ifndef PM_GATHER50_WIDE
-#define PM_GATHER50_WIDE 0
-#endif
-template <int S>
-static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out,
-                                       hipStream_t s, int k, const uint32_t* perm);
-
 hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, float4* out, hipStream_t s,
                          int tag, const uint32_t* perm) {
   if (nq <= 0) return hipSuccess;
   const int n = (int)m->n;
-#if PM_GATHER50_WIDE && !PM_CHECK_VARIANT
-  (void)tag;
-  (void)n;
-  return launch_gather_wide_s<PM_GATHER50_WIDE>(m, qb, nq, out, s, kKNearest, perm);
-#endif
 #if PM_CHECK_VARIANT
   const int g = grid_for(nq, 256);
   if (tag == 1) k_gather_plain<1><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm);

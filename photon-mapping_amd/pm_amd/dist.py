@@ -118,7 +118,7 @@ def allgather_rows_start(t, world: int, dist, pack=None):
     else:
         pack(t, pad[: t.shape[0]])
     if t.device.type == "cuda":
-        out = torch.empty((world * m, t.shape[1]), dtype=t.dtype, device=t.device)
+        out = torch.empty((world * m, cols), dtype=t.dtype, device=t.device)
         work = dist.all_gather_into_tensor(out, pad, async_op=True)
         return _Gathered(work, out, ns, m, world)
     bufs = [torch.empty_like(pad) for _ in range(world)]

@@ -15,4 +15,8 @@ fi
 if [ -n "${LIBS:-}" ]; then
   LIBS="$LIBS" REPS=${REPS:-2} AB_ARGS="${AB_ARGS:-}" bash tools/ab_libs.sh || exit $?
 fi
+if [ "${BENCH:-0}" = 1 ]; then
+  timeout -k 10 400 python -u bench.py ${BENCH_ARGS:---steps 10 --warmup 3} > gpurun_out/bench.log 2>&1 || { echo BENCH_FAILED; tail -20 gpurun_out/bench.log; exit 3; }
+  tail -1 gpurun_out/bench.log
+fi
 echo call-done
