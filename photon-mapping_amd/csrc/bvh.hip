@@ -294,14 +294,6 @@ __device__ __forceinline__ float box_area(const float b[6]) {
   return dx * dy + dy * dz + dz * dx;
 }
 
-// PM_BVH_PAIRS: binary node b with two triangle children stays a leaf; until
-// k_leaf_place lays the triangles out it is coded kPairCode - b
-constexpr int kPairCode = -(1 << 30);
-__device__ __forceinline__ bool is_pair(const float4* __restrict__ bin, int b) {
-  const int4 c = *reinterpret_cast<const int4*>(&bin[4 * b + 3]);
-  return c.x < 0 && c.y < 0;
-}
-
 __global__ void k_collapse_open(const float4* __restrict__ bin, const int2* __restrict__ frontier, int nf,
                                 float4* __restrict__ q, uint32_t* __restrict__ cnt) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
@@ -321,7 +313,7 @@ __global__ void k_collapse_open(const float4* __restrict__ bin, const int2* __re
     float barea = -1.0f;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-      if (c < m && code[c] >= 0 && !(PM_BVH_PAIRS && is_pair(bin, code[c]))) {
+      if (c < m && code[c] >= 0) {
         const float a = box_area(box[c]);
         if (a > barea) barea = a, best = c;
       }
@@ -348,7 +340,6 @@ __global__ void k_collapse_open(const float4* __restrict__ bin, const int2* __re
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     const bool used = c < m;
-    if (PM_BVH_PAIRS && used && code[c] >= 0 && is_pair(bin, code[c])) code[c] = kPairCode - code[c];
     if (used && code[c] >= 0) internal++;
 #pragma unroll
     for (int k = 0; k < 6; k++) qn[4 * k + c] = used ? box[c][k] : 0.0f;   // k: lo.x hi.x lo.y hi.y lo.z hi.z
@@ -378,177 +369,8 @@ __global__ void k_collapse_link(const int2* __restrict__ frontier, int nf, const
   *cp = c;
 }
 
-// ---------------------------------------------------------------- BVH8 (quantised)
-// PM_BVH_WIDTH 8: the same greedy collapse opens 6 times (8 children) and the
-// node stores its children's boxes as 8-bit offsets from the node's corner p in
-// units of a per-axis power of two s (128 B, one cache line):
-//   f4[0]    p.xyz, exponent bytes (IEEE biased) of s.x | s.y << 8 | s.z << 16
-//   f4[1..2] child codes [8] (>= 0 node, kBvhEmpty unused, else ~triangle slot)
-//   f4[3..5] per axis: qlo[8] bytes (2 dwords), qhi[8] bytes (2 dwords)
-// The decoded box p + q * s (q * s exact, one rounding) CONTAINS the padded child
-// box: each q is stepped outwards until the float decode does, so culling stays
-// conservative and the traversal's argmin result is unchanged.
+// decoded plane of a quantised box: p + q s (q s exact, one rounding)
 __device__ __forceinline__ float q_decode(float p, uint32_t q, float sc) { return p + (float)q * sc; }
-
-__global__ void k_collapse_open8(const float4* __restrict__ bin, const int2* __restrict__ frontier, int nf,
-                                 float4* __restrict__ q, uint32_t* __restrict__ cnt) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= nf) return;
-  const int2 fr = frontier[f];
-  int code[8];
-  float box[8][6];
-  const float* nb = reinterpret_cast<const float*>(&bin[4 * fr.x]);
-  const int4 c2 = *reinterpret_cast<const int4*>(&bin[4 * fr.x + 3]);
-  code[0] = c2.x;
-  code[1] = c2.y;
-#pragma unroll
-  for (int k = 0; k < 6; k++) box[0][k] = nb[k], box[1][k] = nb[6 + k];
-  int m = 2;
-  for (int it = 0; it < 6; it++) {
-    int best = -1;
-    float barea = -1.0f;
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      if (c < m && code[c] >= 0) {
-        const float a = box_area(box[c]);
-        if (a > barea) barea = a, best = c;
-      }
-    }
-    if (best < 0) break;
-    const float* ob = reinterpret_cast<const float*>(&bin[4 * code[best]]);
-    const int4 oc = *reinterpret_cast<const int4*>(&bin[4 * code[best] + 3]);
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      if (c == best) {
-        code[c] = oc.x;
-#pragma unroll
-        for (int k = 0; k < 6; k++) box[c][k] = ob[k];
-      } else if (c == m) {
-        code[c] = oc.y;
-#pragma unroll
-        for (int k = 0; k < 6; k++) box[c][k] = ob[6 + k];
-      }
-    }
-    m++;
-  }
-  // node corner and per-axis scale
-  float p[3], hi[3];
-  uint32_t eb[3];
-#pragma unroll
-  for (int a = 0; a < 3; a++) {
-    p[a] = box[0][2 * a];
-    hi[a] = box[0][2 * a + 1];
-#pragma unroll
-    for (int c = 1; c < 8; c++) {
-      if (c < m) {
-        p[a] = fminf(p[a], box[c][2 * a]);
-        hi[a] = fmaxf(hi[a], box[c][2 * a + 1]);
-      }
-    }
-    const double ext = (double)hi[a] - (double)p[a];
-    int e = 1;   // biased exponent of s
-    if (ext > 0.0) {
-      int k;
-      frexp(ext / 255.0, &k);   // ext / 255 < 2^k
-      e = k + 127;
-    }
-    e = e < 1 ? 1 : e;
-    while (e < 254 && q_decode(p[a], 255u, __uint_as_float((uint32_t)e << 23)) < hi[a]) e++;
-    eb[a] = (uint32_t)e;
-  }
-  uint32_t qw[3][4] = {};   // per axis: qlo dwords 0,1; qhi dwords 2,3
-  uint32_t internal = 0;
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    const bool used = c < m;
-    if (used && code[c] >= 0) internal++;
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-      uint32_t ql = 0, qh = 0;
-      if (used) {
-        const float sc = __uint_as_float(eb[a] << 23);
-        const double inv = 1.0 / (double)sc;
-        double dl = floor(((double)box[c][2 * a] - (double)p[a]) * inv);
-        double dh = ceil(((double)box[c][2 * a + 1] - (double)p[a]) * inv);
-        ql = (uint32_t)fmin(fmax(dl, 0.0), 255.0);
-        qh = (uint32_t)fmin(fmax(dh, 0.0), 255.0);
-        while (ql > 0 && q_decode(p[a], ql, sc) > box[c][2 * a]) ql--;
-        while (qh < 255 && q_decode(p[a], qh, sc) < box[c][2 * a + 1]) qh++;
-      }
-      qw[a][c >> 2] |= ql << (8 * (c & 3));
-      qw[a][2 + (c >> 2)] |= qh << (8 * (c & 3));
-    }
-  }
-  float4* qn = &q[8 * (int64_t)fr.y];
-  qn[0] = make_float4(p[0], p[1], p[2], __uint_as_float(eb[0] | eb[1] << 8 | eb[2] << 16));
-  int* cc = reinterpret_cast<int*>(&qn[1]);
-#pragma unroll
-  for (int c = 0; c < 8; c++) cc[c] = c < m ? code[c] : kBvhEmpty;   // patched by k_collapse_link8
-#pragma unroll
-  for (int a = 0; a < 3; a++)
-    qn[3 + a] = make_float4(__uint_as_float(qw[a][0]), __uint_as_float(qw[a][1]), __uint_as_float(qw[a][2]),
-                            __uint_as_float(qw[a][3]));
-  qn[6] = make_float4(0.f, 0.f, 0.f, 0.f);
-  qn[7] = make_float4(0.f, 0.f, 0.f, 0.f);
-  cnt[f] = internal;
-}
-
-__global__ void k_collapse_link8(const int2* __restrict__ frontier, int nf, const uint32_t* __restrict__ off,
-                                 int base, float4* __restrict__ q, int2* __restrict__ next) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= nf) return;
-  const int2 fr = frontier[f];
-  int* cc = reinterpret_cast<int*>(&q[8 * (int64_t)fr.y + 1]);
-  int o = (int)off[f];
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const int c = cc[k];
-    if (c >= 0) {
-      next[o] = make_int2(c, base + o);
-      cc[k] = base + o;
-      o++;
-    }
-  }
-}
-
-// PM_BVH_PAIRS: triangles re-laid so that every leaf's triangles are contiguous
-// (node order), leaf codes ~(slot << 1 | count - 1)
-__device__ __forceinline__ int leaf_tris(int c) { return c == kBvhEmpty || c >= 0 ? 0 : (c <= kPairCode ? 2 : 1); }
-__global__ void k_leaf_count(const float4* __restrict__ q, int nn, uint32_t* __restrict__ cnt) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nn) return;
-  const int4 c = *reinterpret_cast<const int4*>(&q[8 * (int64_t)i + 6]);
-  cnt[i] = leaf_tris(c.x) + leaf_tris(c.y) + leaf_tris(c.z) + leaf_tris(c.w);
-}
-__global__ void k_leaf_place(float4* __restrict__ q, int nn, const uint32_t* __restrict__ off,
-                             const float4* __restrict__ bin, const float4* __restrict__ tri,
-                             float4* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nn) return;
-  int4* cp = reinterpret_cast<int4*>(&q[8 * (int64_t)i + 6]);
-  int4 c4 = *cp;
-  int* cc = reinterpret_cast<int*>(&c4);
-  int next = (int)off[i];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int c = cc[k];
-    const int n = leaf_tris(c);
-    if (n == 0) continue;
-    int src[2];
-    if (n == 1) {
-      src[0] = ~c;
-    } else {
-      const int4 bc = *reinterpret_cast<const int4*>(&bin[4 * (kPairCode - c) + 3]);
-      src[0] = ~bc.x;
-      src[1] = ~bc.y;
-    }
-    for (int t = 0; t < n; t++)
-      for (int v = 0; v < 3; v++) out[3 * (int64_t)(next + t) + v] = tri[3 * (int64_t)src[t] + v];
-    cc[k] = ~((next << 1) | (n - 1));
-    next += n;
-  }
-  *cp = c4;
-}
 
 // PM_BVH_Q4: the float BVH4 node (8 x float4) -> 64 B (4 x float4, see
 // traverse_step4): corner p = min of the used children's lo, per-axis scale
@@ -613,12 +435,10 @@ static hipError_t collapse_bvh(const float4* bin, int nbin, pm_scene* sc, hipStr
   int2 *cur = fa.p, *nxt = fb.p;
   while (nf > 0) {
     depth++;
-    if (kBvhWidth == 8) k_collapse_open8<<<grid_for(nf, 256), 256, 0, s>>>(bin, cur, nf, sc->nodes.p, cnt.p);
-    else k_collapse_open<<<grid_for(nf, 256), 256, 0, s>>>(bin, cur, nf, sc->nodes.p, cnt.p);
+    k_collapse_open<<<grid_for(nf, 256), 256, 0, s>>>(bin, cur, nf, sc->nodes.p, cnt.p);
     PM_HIP_TRY(hipGetLastError());
     PM_HIP_TRY(exclusive_scan_u32(cnt.p, off.p, nf, total.p, s));
-    if (kBvhWidth == 8) k_collapse_link8<<<grid_for(nf, 256), 256, 0, s>>>(cur, nf, off.p, alloc, sc->nodes.p, nxt);
-    else k_collapse_link<<<grid_for(nf, 256), 256, 0, s>>>(cur, nf, off.p, alloc, sc->nodes.p, nxt);
+    k_collapse_link<<<grid_for(nf, 256), 256, 0, s>>>(cur, nf, off.p, alloc, sc->nodes.p, nxt);
     PM_HIP_TRY(hipGetLastError());
     uint32_t t = 0;
     PM_HIP_TRY(hipMemcpyAsync(&t, total.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -629,23 +449,6 @@ static hipError_t collapse_bvh(const float4* bin, int nbin, pm_scene* sc, hipStr
   }
   sc->nnodes = alloc;
   sc->depth = depth;
-  if (PM_BVH_PAIRS && kBvhWidth == 4) {
-    DevBuf<uint32_t> lc(alloc), lo(alloc), lt(1);
-    if (!lc.p || !lo.p || !lt.p) return hipErrorOutOfMemory;
-    k_leaf_count<<<grid_for(alloc, 256), 256, 0, s>>>(sc->nodes.p, alloc, lc.p);
-    PM_HIP_TRY(hipGetLastError());
-    PM_HIP_TRY(exclusive_scan_u32(lc.p, lo.p, alloc, lt.p, s));
-    uint32_t nt = 0;
-    PM_HIP_TRY(hipMemcpyAsync(&nt, lt.p, 4, hipMemcpyDeviceToHost, s));
-    PM_HIP_TRY(hipStreamSynchronize(s));
-    DevBuf<float4> laid((size_t)3 * nt);
-    if (!laid.p) return hipErrorOutOfMemory;
-    k_leaf_place<<<grid_for(alloc, 256), 256, 0, s>>>(sc->nodes.p, alloc, lo.p, bin, sc->tri.p, laid.p);
-    PM_HIP_TRY(hipGetLastError());
-    PM_HIP_TRY(hipStreamSynchronize(s));
-    std::swap(sc->tri.p, laid.p);
-    std::swap(sc->tri.n, laid.n);
-  }
   if (kBvhQ4) {
     DevBuf<float4> qn((size_t)4 * alloc);
     if (!qn.p) return hipErrorOutOfMemory;

@@ -670,9 +670,7 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     for (int d = 0; d < 3; d++) {
       uint64_t k = tid < S ? (uint64_t)orderable_key(coord_of(me, d)) << 32 | (uint32_t)__float_as_int(me.w) : ~0ull;
       int v = tid;
-#ifndef PM_KS_NOSORT   // timing diagnostic only: wrong trees
       block_bitonic(k, v, n2, kx, tag);
-#endif
       __syncthreads();   // buf[2] written; every exchange read
       const float4 x = tid < S ? buf[2][v] : me;
       if (d == 2) __syncthreads();

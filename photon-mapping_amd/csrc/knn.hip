@@ -603,16 +603,15 @@ constexpr int kGatherBox = PM_GATHER_BOX;
 #define PM_BOX_AFTER 512
 #endif
 constexpr int kBoxAfter = PM_BOX_AFTER;
-#ifndef PM_KNN_STATS
-#define PM_KNN_STATS 0   // stats library only: walk iterations of the k = 50 gather
-#endif
-#if PM_KNN_STATS
-// [tag][leaders, followers, retry lanes][waves, iterations, max iterations]
-__device__ unsigned long long g_knn_stats[2][3][4];
-#endif
 
 #ifndef PM_GATHER_XCD
 #define PM_GATHER_XCD 0
+#endif
+#ifndef PM_GATHER_CHUNKS
+#define PM_GATHER_CHUNKS 1
+#endif
+#ifndef PM_GATHER_CHUNK_MIN
+#define PM_GATHER_CHUNK_MIN 1024   // leaders per chunk below which the gather runs unchunked
 #endif
 // bijective blockIdx remap: blocks b with equal b % 8 (one XCD, as the
 // dispatcher deals them) get consecutive logical ids (cdna_hip_programming T1)
@@ -701,7 +700,10 @@ template <int TAG, bool LEADERS, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && (kGatherBox == 1 || kGatherBox == 2) ? 3 : 4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
-    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx) {
+    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx, int64_t t0,
+    int64_t t1) {
+  // lanes [t0, t1) of the launch's kind (leader index / follower index): one
+  // chunk of the pipelined gather (launch_gather)
   __shared__ double lq[(kGatherQL + 1) * 256];
   const float R2 = kKMaxDistance * kKMaxDistance;
   // follower launch with a leader budget: the first nretry_blocks workgroups
@@ -720,9 +722,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
     valid = e < *nretry;
     r = valid ? (int64_t)retry[e] : 0;
   } else {
-    const int64_t t = ((int64_t)bid - nrb) * blockDim.x + threadIdx.x;
+    const int64_t t = t0 + ((int64_t)bid - nrb) * blockDim.x + threadIdx.x;
     r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
-    valid = r < nq;
+    valid = t < t1 && r < nq;
   }
   if (redo_lane && ballot(valid) == 0) return;   // wave-uniform: no retry entry for this wave
   const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
@@ -745,8 +747,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
   }
   double list[kKNearest];
   bool aborted;
-  int knn_it = 0;
-  int* const itp = PM_KNN_STATS ? &knn_it : nullptr;
+  int* const itp = nullptr;
   if (kGatherBox == 2 || (kGatherBox == 1 && LEADERS) || (kGatherBox == 3 && !LEADERS)) {
     aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0, kBoxAfter>(
         nodes, n, q, cut, valid, list, lq + threadIdx.x, 256, bx, itp);
@@ -757,14 +758,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
     aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0>(nodes, n, q, cut, valid, list,
                                                                                      lq + threadIdx.x, 256, {}, itp);
   }
-#if PM_KNN_STATS
-  if ((threadIdx.x & 63) == 0) {
-    const int sl = LEADERS ? 0 : (redo_lane ? 2 : 1);
-    atomicAdd(&g_knn_stats[TAG][sl][0], 1ull);
-    atomicAdd(&g_knn_stats[TAG][sl][1], (unsigned long long)knn_it);
-    atomicMax(&g_knn_stats[TAG][sl][2], (unsigned long long)knn_it);
-  }
-#endif
   if (valid && !aborted) {
     const bool full = gkey_word(list[kKNearest - 1]) != kNoWord;
     const v3 f = radiance_g(list, payload, qq.w, full ? gkey_d2(list[kKNearest - 1]) : R2);
@@ -868,9 +861,9 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
 #else
   const int64_t nl = (nq + kSeedStride - 1) / kSeedStride;   // leaders: walk ranks 0, S, 2S, ...
   DevBuf<float4> lead(nl);
-  DevBuf<uint32_t> retry(kLeaderBudget > 0 ? nl : 0), nretry(kLeaderBudget > 0 ? 1 : 0);
+  DevBuf<uint32_t> retry(kLeaderBudget > 0 ? nl : 0), nretry(kLeaderBudget > 0 ? PM_GATHER_CHUNKS : 0);
   if (!lead.p || (kLeaderBudget > 0 && (!retry.p || !nretry.p))) return hipErrorOutOfMemory;
-  if (kLeaderBudget > 0) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, sizeof(uint32_t), s));
+  if (kLeaderBudget > 0) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, sizeof(uint32_t) * PM_GATHER_CHUNKS, s));
   DevBuf<float4> box(kGatherBox ? 2 * (size_t)std::max<int64_t>(boxed_nodes(n, PM_GATHER_BOX_SKIP), 1) : 0);
   BoxView bx;
   hipEvent_t box_done = nullptr;
@@ -929,49 +922,86 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
     box_done = nullptr;
     return e;
   };
-  // followers (+ the retry workgroups first, with a leader budget)
-  const int rb = kLeaderBudget > 0 ? grid_for(nl, 256) : 0;   // retry workgroups: one lane per leader
-  const int gl = grid_for(nl, 256), gf = grid_for(nq - nl, 256) + rb;
+  // Pipelined leaders (PM_GATHER_CHUNKS = C > 1): the walk order is cut into
+  // C chunks of whole leader strides; the leader launches run back to back on
+  // a side stream and follower chunk c (+ chunk c's retried leaders at its
+  // head) starts on s as soon as leader chunks c and c + 1 are done (its
+  // queries read the records of leaders jp - 1 .. jp + 2). The leader
+  // launches' last, under-filled rounds then overlap the followers of earlier
+  // chunks instead of idling the GPU before the first follower starts.
+  // C = 1: one leader launch, then one follower launch (rounds 1-3).
+  int C = PM_GATHER_CHUNKS;
+  // small gathers: chunks would under-fill the GPU; every chunk holds >= 2
+  // leaders, so follower chunk c's last records (jp + 2) lie in chunk c + 1
+  if (nl < (int64_t)C * std::max(PM_GATHER_CHUNK_MIN, 2)) C = 1;
+  hipStream_t ls = C > 1 ? side_stream(stream_device(s), 3) : nullptr;
+  if (C > 1 && !ls) C = 1;
+  std::vector<hipEvent_t> evs;
+  struct EvGuard {
+    std::vector<hipEvent_t>& v;
+    ~EvGuard() {
+      for (hipEvent_t e : v) (void)hipEventDestroy(e);
+    }
+  } ev_guard{evs};
+  for (int c = 0; C > 1 && c <= C; c++) {
+    hipEvent_t e = nullptr;
+    PM_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    evs.push_back(e);
+  }
+  if (C > 1) {   // the leader stream starts after everything before this call on s
+    PM_HIP_TRY(hipEventRecord(evs[C], s));
+    PM_HIP_TRY(hipStreamWaitEvent(ls, evs[C], 0));
+  }
+  auto lead_lo = [&](int c) -> int64_t { return nl * c / C; };
+  const int64_t nf = nq - nl;
   // node byte offsets fit 32 bits below 2^28 nodes (saddr loads); larger maps use 64-bit addresses
   const bool wide = PM_FORCE_WIDE || n >= (1 << 28);
-#define PM_LEVELS(T, W)                                                                                          \
-  k_gather_level<T, true, W><<<gl, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, retry.p, \
-                                                nretry.p, 0, bx);                                               \
-  PM_HIP_TRY(hipGetLastError());                                                                                \
-  PM_HIP_TRY(boxes_ready());                                                                                    \
-  if (nq > nl || kLeaderBudget > 0)                                                                             \
-  k_gather_level<T, false, W><<<gf, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, retry.p, \
-                                                 nretry.p, rb, bx)
-  if (tag == 1) {
-    if (wide) {
-      PM_LEVELS(1, true);
-    } else {
-      PM_LEVELS(1, false);
-    }
+  uint32_t* const rt = kLeaderBudget > 0 ? retry.p : nullptr;
+  uint32_t* const nrt = kLeaderBudget > 0 ? nretry.p : nullptr;
+  // one launch of k_gather_level<tag, LEADERS, wide> over lanes [t0, t1);
+  // chunk c's retry list is retry[lead_lo(c) ..], its count nretry[c]
+  auto level = [&](auto leaders, int c, int grid, int rb, int64_t t0, int64_t t1, hipStream_t st) -> hipError_t {
+    constexpr bool L = decltype(leaders)::value;
+    if (grid <= 0) return hipSuccess;
+    uint32_t* const cr = rt ? rt + lead_lo(c) : nullptr;
+    uint32_t* const cn = nrt ? nrt + c : nullptr;
+    const float4 *nd = m->nodes.p, *pl = m->payload.p;
+    if (tag == 1 && wide)
+      k_gather_level<1, L, true><<<grid, 256, 0, st>>>(nd, pl, n, qb, nq, out, perm, lead.p, cr, cn, rb, bx, t0, t1);
+    else if (tag == 1)
+      k_gather_level<1, L, false><<<grid, 256, 0, st>>>(nd, pl, n, qb, nq, out, perm, lead.p, cr, cn, rb, bx, t0, t1);
+    else if (wide)
+      k_gather_level<0, L, true><<<grid, 256, 0, st>>>(nd, pl, n, qb, nq, out, perm, lead.p, cr, cn, rb, bx, t0, t1);
+    else
+      k_gather_level<0, L, false><<<grid, 256, 0, st>>>(nd, pl, n, qb, nq, out, perm, lead.p, cr, cn, rb, bx, t0, t1);
+    return hipGetLastError();
+  };
+  auto launch_leaders = [&](int c, hipStream_t st) -> hipError_t {
+    const int64_t a = lead_lo(c), b = lead_lo(c + 1);
+    return level(std::true_type{}, c, grid_for(b - a, 256), 0, a, b, st);
+  };
+  auto launch_followers = [&](int c) -> hipError_t {
+    const int64_t a = lead_lo(c), b = lead_lo(c + 1);
+    // follower index t <-> rank (t / (S - 1)) S + 1 + t % (S - 1): chunk c's ranks [a S, b S)
+    const int64_t f0 = std::min(a * (kSeedStride - 1), nf), f1 = c == C - 1 ? nf : std::min(b * (kSeedStride - 1), nf);
+    const int rb = kLeaderBudget > 0 ? grid_for(b - a, 256) : 0;   // chunk c's retried leaders: one lane each
+    return level(std::false_type{}, c, grid_for(f1 - f0, 256) + rb, rb, f0, f1, s);
+  };
+  if (C == 1) {
+    PM_HIP_TRY(launch_leaders(0, s));
+    PM_HIP_TRY(boxes_ready());
+    if (nf > 0 || kLeaderBudget > 0) PM_HIP_TRY(launch_followers(0));
   } else {
-    if (wide) {
-      PM_LEVELS(0, true);
-    } else {
-      PM_LEVELS(0, false);
+    for (int c = 0; c < C; c++) {
+      PM_HIP_TRY(launch_leaders(c, ls));
+      PM_HIP_TRY(hipEventRecord(evs[c], ls));
+    }
+    PM_HIP_TRY(boxes_ready());
+    for (int c = 0; c < C; c++) {
+      PM_HIP_TRY(hipStreamWaitEvent(s, evs[std::min(c + 1, C - 1)], 0));
+      PM_HIP_TRY(launch_followers(c));
     }
   }
-#undef PM_LEVELS
-#if PM_KNN_STATS
-  {
-    PM_HIP_TRY(hipStreamSynchronize(s));
-    unsigned long long st[2][3][4];
-    uint32_t nr = 0;
-    PM_HIP_TRY(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_knn_stats), sizeof(st)));
-    PM_HIP_TRY(hipMemcpy(&nr, nretry.p, sizeof(nr), hipMemcpyDeviceToHost));
-    const char* nm[3] = {"leaders", "followers", "retry"};
-    for (int j = 0; j < 3; j++)
-      fprintf(stderr, "[gather50 tag=%d n=%d nq=%lld %s] waves %llu iters/wave %.1f max %llu (retried leaders %u of %lld)\n",
-              tag, n, (long long)nq, nm[j], st[tag][j][0], st[tag][j][1] / (double)std::max(st[tag][j][0], 1ull),
-              st[tag][j][2], nr, (long long)nl);
-    static const unsigned long long zero[2][3][4] = {};
-    PM_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_knn_stats), zero, sizeof(zero)));
-  }
-#endif
   return hipGetLastError();
 #endif
 }
@@ -1130,18 +1160,6 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, B
   nd = ndn;
 }
 
-#ifndef PM_WIDE_STATS
-#define PM_WIDE_STATS 0
-#endif
-#ifndef PM_WIDE_DIAG
-#define PM_WIDE_DIAG 0   // timing diagnostics only (wrong results): 1 no final sorts, 2 no sorts at all,
-                         // 3 no sorts, an overflowing row stops its lane
-#endif
-#if PM_WIDE_STATS
-// stats library only: [launch][0 groups, 1 iterations, 2 max iterations per group,
-// 3 flushes, 4 candidates, 5 valid lanes, 6 final keys]
-__device__ unsigned long long g_wide_stats[2][8];
-#endif
 
 // Leader step budget of the wide gather (wave iterations; 0: none): the
 // leader launch is a few thousand waves on an otherwise idle GPU, so its length
@@ -1215,13 +1233,7 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
       LeanWalk w;
       w.start(cut, valid);
       float4 nd = node1<WIDE>(nodes, 1), ba = bx.box[0], bb = bx.box[1];
-#if PM_WIDE_STATS
-      unsigned long long it = 0, fl = 0, nc = 0;
-#endif
       for (;;) {
-#if PM_WIDE_STATS
-        const int c0 = cnt;
-#endif
         collect_step<WIDE>(nodes, bx, (uint32_t)n, q, tail, w, nd, ba, bb, row, cnt, stage);
         if (LEADERS && kWideLeaderBudget > 0 && ++it_b == kWideLeaderBudget) {
           aborted = w.walking;   // redone at the head of the follower launch
@@ -1229,23 +1241,17 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
         }
         uint64_t full = ballot(cnt == CAP);
         const uint64_t full0 = full;
-#if PM_WIDE_STATS
-        it++;
-        fl += __popcll(full);
-        nc += cnt - c0;
-#endif
         if (full) {   // flush: keep each full row's k smallest, tighten its cut-off
           fence_wave();
           while (full) {
             const int l = __ffsll((long long)full) - 1;
             full &= full - 1;
-            const double tl = PM_WIDE_DIAG >= 2 ? tail : row_sort<S>(wrows + l * CAP, CAP, k, lane);
+            const double tl = row_sort<S>(wrows + l * CAP, CAP, k, lane);
             if (lane == l) {
               cnt = k;
               tail = tl;
               flushed = true;
               w.bound = gkey_d2(tl);
-              if (PM_WIDE_DIAG == 3) w.walking = false;   // diagnostic: an overflowing lane stops
             }
           }
           fence_wave();
@@ -1258,26 +1264,12 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
         }
         if (ballot(w.walking) == 0) break;
       }
-#if PM_WIDE_STATS
-      atomicAdd(&g_wide_stats[LEADERS][4], nc);
-      const uint64_t vm = ballot(valid);
-      if (lane == 0) {
-        atomicAdd(&g_wide_stats[LEADERS][0], 1ull);
-        atomicAdd(&g_wide_stats[LEADERS][1], it);
-        atomicMax(&g_wide_stats[LEADERS][2], it);
-        atomicAdd(&g_wide_stats[LEADERS][3], fl);
-        atomicAdd(&g_wide_stats[LEADERS][5], (unsigned long long)__popcll(vm));
-      }
-#endif
     }
-#if PM_WIDE_STATS
-    atomicAdd(&g_wide_stats[LEADERS][6], (unsigned long long)cnt);
-#endif
     // final sort of every row: its first min(cnt, k) keys in (d^2, index) order
     spill_stage(cnt);
     fence_wave();
 
-    uint64_t live = PM_WIDE_DIAG ? 0 : ballot(cnt > 0 && !aborted);
+    uint64_t live = ballot(cnt > 0 && !aborted);
     while (live) {
       const int l = __ffsll((long long)live) - 1;
       live &= live - 1;
@@ -1356,12 +1348,6 @@ static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb,
   BoxView bx;
   bx.box = box.p;
   bx.nbox = (uint32_t)nbox;
-#if PM_WIDE_STATS
-  {
-    static const unsigned long long zero[16] = {};
-    PM_HIP_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_wide_stats), zero, sizeof(zero), 0, hipMemcpyHostToDevice, s));
-  }
-#endif
   const bool wide = PM_FORCE_WIDE || n >= (1 << 28);
 #define PM_WIDE_LAUNCH(W)                                                                                          \
   k_gather_wide<0, true, W, S><<<(int)std::min<int64_t>(wg, (nl + 255) / 256), 256, 0, s>>>(                     \
@@ -1379,20 +1365,6 @@ static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb,
     PM_WIDE_LAUNCH(false)
   }
 #undef PM_WIDE_LAUNCH
-#if PM_WIDE_STATS
-  {
-    PM_HIP_TRY(hipStreamSynchronize(s));
-    unsigned long long st[2][8];
-    PM_HIP_TRY(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_wide_stats), sizeof(st)));
-    for (int L = 1; L >= 0; L--)
-      fprintf(stderr,
-              "[wide k=%d n=%d %s] groups %llu lanes %llu iters/group %.1f max %llu flushes/lane %.3f candidates/lane %.1f "
-              "final keys/lane %.1f\n",
-              k, n, L ? "leaders" : "followers", st[L][0], st[L][5], st[L][1] / (double)std::max(st[L][0], 1ull),
-              st[L][2], st[L][3] / (double)std::max(st[L][5], 1ull), st[L][4] / (double)std::max(st[L][5], 1ull),
-              st[L][6] / (double)std::max(st[L][5], 1ull));
-  }
-#endif
   return hipStreamSynchronize(s);   // rows / leader records / boxes are freed on return
 }
 

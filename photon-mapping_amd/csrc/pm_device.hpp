@@ -298,26 +298,19 @@ constexpr int kStackDepth = PM_STACK_DEPTH;
 #define PM_WAVES_ATTR(w) __attribute__((amdgpu_waves_per_eu((w) > 0 ? (w) : 1, (w) > 0 ? (w) : 10)))
 // PM_NO_SPILL: LDS stack only (no private scratch in any traversal kernel);
 // rays deeper than kStackDepth report PM_ERR_OVERFLOW. A/B and diagnostics.
-// BVH width (build knob, library-wide): 4 = 128-B float boxes, 8 = 128-B
-// quantised boxes (bvh.hip, k_collapse_open8). Width 8 passes the GPU suite
-// bitwise but measured slower on config 3: trace 33.3 -> 44.3 ms, paths 18.5 ->
-// 26.5 ms (79 VGPRs, 6 waves/SIMD; forced to 8 waves: 45.8 / 27.4 ms). A width-W BVH of depth D needs at
-// most (W - 1)(D - 1) stack entries: 64 in total for W = 4 (D <= 22), 128 for
-// W = 8 (D <= 19).
-#ifndef PM_BVH_WIDTH
-#define PM_BVH_WIDTH 4
-#endif
-constexpr int kBvhWidth = PM_BVH_WIDTH;
-static_assert(kBvhWidth == 4 || kBvhWidth == 8, "PM_BVH_WIDTH is 4 or 8");
+// BVH4 (4 children per node). A BVH4 of depth D needs at most 3(D - 1) stack
+// entries: 64 in total for D <= 22. (Round 3 measured, and removed in round 4,
+// an 8-wide quantised BVH: bitwise on the GPU suite but slower on config 3,
+// trace 33.3 -> 44.3 ms, paths 18.5 -> 26.5 ms at 6 waves/SIMD.)
 // PM_BVH_Q4 (build knob, width 4): the float BVH4 is converted to 64-B nodes
 // with 8-bit child boxes (bvh.hip, k_quantize4): half the bytes and 4 instead
 // of 7 16-B loads per visited node, for a per-plane fma decode.
 #ifndef PM_BVH_Q4
 #define PM_BVH_Q4 1
 #endif
-constexpr bool kBvhQ4 = PM_BVH_Q4 && kBvhWidth == 4;
+constexpr bool kBvhQ4 = PM_BVH_Q4;
 constexpr int kNodeF4 = kBvhQ4 ? 4 : 8;   // float4 per node
-constexpr int kStackTotal = kBvhWidth == 8 ? 128 : 64;
+constexpr int kStackTotal = 64;
 #ifdef PM_NO_SPILL
 constexpr int kSpillDepth = 0;
 #else
@@ -361,62 +354,21 @@ __device__ __forceinline__ bool leaf_hit(const float4 a, const float4 b, const f
   return false;
 }
 
-// PM_BVH_PAIRS (build knob): a binary node whose two children are triangles
-// becomes one leaf of two contiguous triangles (bvh.hip, k_leaf_place); leaf
-// codes are then ~(slot << 1 | count - 1). Off: ~slot, one triangle per leaf.
-#ifndef PM_BVH_PAIRS
-#define PM_BVH_PAIRS 0
-#endif
-static_assert(!(PM_BVH_PAIRS && PM_BVH_WIDTH == 8), "paired leaves are laid out for the BVH4 collapse only");
+// one triangle per leaf: code ~slot (round 3's two-triangle leaves measured
+// slower, trace 29.6 -> 30.3 ms, and were removed in round 4)
 template <bool ANY>
 __device__ __forceinline__ bool leaf_test(const DevScene& S, const Ray& r, float tmin, float tmax, int code,
                                           HitInfo& h) {
-  if (PM_BVH_PAIRS) {
-    const int v = ~code, slot = v >> 1;
-    const bool h0 =
-        leaf_hit<ANY>(S.tri[3 * slot + 0], S.tri[3 * slot + 1], S.tri[3 * slot + 2], r, tmin, tmax, slot, h);
-    if (ANY && h0) return true;
-    if (v & 1) {
-      const int s1 = slot + 1;
-      const bool h1 = leaf_hit<ANY>(S.tri[3 * s1 + 0], S.tri[3 * s1 + 1], S.tri[3 * s1 + 2], r, tmin, tmax, s1, h);
-      return h0 || h1;
-    }
-    return h0;
-  }
   const int slot = ~code;
   return leaf_hit<ANY>(S.tri[3 * slot + 0], S.tri[3 * slot + 1], S.tri[3 * slot + 2], r, tmin, tmax, slot, h);
 }
 
-// PM_LEAF_BATCH (build knob): 1 tests a node's hit leaves one after another
-// (each leaf's triangle load waits for the previous test); 2 / 4 issue the
-// loads of 2 / 4 hit leaves before testing them, so they overlap. Measured on
-// config 3: paths 22.8 -> 25.0 / 24.6 ms, trace 42.1 -> 42.4 / 43.6 ms (the
-// extra VGPRs drop the ray kernels from 7-8 to 5-6 waves per SIMD).
-#ifndef PM_LEAF_BATCH
-#define PM_LEAF_BATCH 1
-#endif
 // PM_LEAF_COMPACT (build knob): test the hit leaves in compacted rounds.
+// (Issuing the triangle loads of 2 / 4 hit leaves before testing them cost
+// VGPRs and measured slower, paths 22.8 -> 25.0 / 24.6 ms; removed in round 4.)
 #ifndef PM_LEAF_COMPACT
 #define PM_LEAF_COMPACT 1
 #endif
-template <bool ANY, int NB>
-__device__ __forceinline__ bool leaf_batch(const DevScene& S, const Ray& r, float tmin, float tmax, const bool (&lv)[NB],
-                                           const int (&code)[NB], HitInfo& h) {
-  float4 a[NB], b[NB], c[NB];
-#pragma unroll
-  for (int k = 0; k < NB; k++) {
-    if (lv[k]) {
-      const int slot = ~code[k];
-      a[k] = S.tri[3 * slot + 0];
-      b[k] = S.tri[3 * slot + 1];
-      c[k] = S.tri[3 * slot + 2];
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < NB; k++)
-    if (lv[k] && leaf_hit<ANY>(a[k], b[k], c[k], r, tmin, tmax, ~code[k], h) && ANY) return true;
-  return false;
-}
 
 // One traversal step: visit `node` (slab-test its 4 children, test its leaf
 // children, push the internal hits near-to-far and continue with the nearest,
@@ -480,16 +432,7 @@ __device__ __forceinline__ bool traverse_step4(const DevScene& S, const Ray& r, 
   }
   }
   // leaves first: a hit shrinks the limit applied to the internal children
-  if (PM_LEAF_BATCH == 4) {
-    const bool lv[4] = {b0 && ch.x < 0, b1 && ch.y < 0, b2 && ch.z < 0, b3 && ch.w < 0};
-    const int cd[4] = {ch.x, ch.y, ch.z, ch.w};
-    if (leaf_batch<ANY, 4>(S, r, tmin, tmax, lv, cd, h)) return true;
-  } else if (PM_LEAF_BATCH == 2) {
-    const bool lv0[2] = {b0 && ch.x < 0, b1 && ch.y < 0}, lv1[2] = {b2 && ch.z < 0, b3 && ch.w < 0};
-    const int cd0[2] = {ch.x, ch.y}, cd1[2] = {ch.z, ch.w};
-    if (leaf_batch<ANY, 2>(S, r, tmin, tmax, lv0, cd0, h)) return true;
-    if (leaf_batch<ANY, 2>(S, r, tmin, tmax, lv1, cd1, h)) return true;
-  } else if (PM_LEAF_COMPACT) {
+  if (PM_LEAF_COMPACT) {
     // hit leaves compacted to the front: round k tests every lane's k-th hit
     // leaf, and the wave runs max(#hit leaves) rounds (order-free: argmin)
     const bool f0 = b0 && ch.x < 0, f1 = b1 && ch.y < 0, f2 = b2 && ch.z < 0, f3 = b3 && ch.w < 0;
@@ -550,113 +493,10 @@ __device__ __forceinline__ bool traverse_step4(const DevScene& S, const Ray& r, 
   return false;
 }
 
-// compare-and-swap on (t, code) pairs, ascending t
-__device__ __forceinline__ void cas8(float (&k)[8], int (&c)[8], int i, int j) {
-  const bool sw = k[j] < k[i];
-  const float ti = sw ? k[j] : k[i], tj = sw ? k[i] : k[j];
-  const int ci = sw ? c[j] : c[i], cj = sw ? c[i] : c[j];
-  k[i] = ti, k[j] = tj, c[i] = ci, c[j] = cj;
-}
-
-// BVH8 step (quantised node, see k_collapse_open8): decode the 8 child boxes in
-// ray-t space (t = q * (s * inv) + (p - o) * inv, one fma per plane; the boxes
-// are padded, so this culling is conservative like slab_fma), test the hit
-// leaves in compacted rounds, push the internal hits near-to-far (19-comparator
-// network) and continue with the nearest, or pop.
-template <bool ANY>
-__device__ __forceinline__ bool traverse_step8(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
-                                               int stride, int* spill, int& node, int& sp, HitInfo& h,
-                                               int* overflow) {
-  const float4* qn = S.nodes + 8 * (int64_t)node;
-  const float4 h0 = qn[0];
-  const int4 ca = *reinterpret_cast<const int4*>(&qn[1]);
-  const int4 cb = *reinterpret_cast<const int4*>(&qn[2]);
-  const uint4 qx = *reinterpret_cast<const uint4*>(&qn[3]);
-  const uint4 qy = *reinterpret_cast<const uint4*>(&qn[4]);
-  const uint4 qz = *reinterpret_cast<const uint4*>(&qn[5]);
-  const uint32_t eb = __float_as_uint(h0.w);
-  const float ax = __uint_as_float((eb & 0xFFu) << 23) * r.inv.x;
-  const float ay = __uint_as_float(((eb >> 8) & 0xFFu) << 23) * r.inv.y;
-  const float az = __uint_as_float(((eb >> 16) & 0xFFu) << 23) * r.inv.z;
-  const float bx = (h0.x - r.o.x) * r.inv.x, by = (h0.y - r.o.y) * r.inv.y, bz = (h0.z - r.o.z) * r.inv.z;
-  const float lim = (ANY || h.slot < 0) ? tmax * 1.00001f : h.t * 1.00001f;
-  int code[8] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w};
-  float tn[8];
-  uint32_t hitm = 0, leafm = 0;
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    const int sh = 8 * (c & 3);
-    const float lx = (float)(((c < 4 ? qx.x : qx.y) >> sh) & 0xFFu), hx = (float)(((c < 4 ? qx.z : qx.w) >> sh) & 0xFFu);
-    const float ly = (float)(((c < 4 ? qy.x : qy.y) >> sh) & 0xFFu), hy = (float)(((c < 4 ? qy.z : qy.w) >> sh) & 0xFFu);
-    const float lz = (float)(((c < 4 ? qz.x : qz.y) >> sh) & 0xFFu), hz = (float)(((c < 4 ? qz.z : qz.w) >> sh) & 0xFFu);
-    const float t0x = __builtin_fmaf(lx, ax, bx), t1x = __builtin_fmaf(hx, ax, bx);
-    const float t0y = __builtin_fmaf(ly, ay, by), t1y = __builtin_fmaf(hy, ay, by);
-    const float t0z = __builtin_fmaf(lz, az, bz), t1z = __builtin_fmaf(hz, az, bz);
-    tn[c] = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
-    const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), lim));
-    const bool b = tn[c] <= tf && code[c] != kBvhEmpty;
-    hitm |= b ? (1u << c) : 0u;
-    leafm |= (b && code[c] < 0) ? (1u << c) : 0u;
-  }
-  // hit leaves in compacted rounds: round k tests every lane's k-th hit leaf
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    if (__ballot(leafm != 0) == 0) break;
-    if (leafm) {
-      const int c = __builtin_ctz(leafm);
-      leafm &= leafm - 1;
-      int cd = code[0];
-#pragma unroll
-      for (int j = 1; j < 8; j++) cd = c == j ? code[j] : cd;
-      if (leaf_test<ANY>(S, r, tmin, tmax, cd, h) && ANY) return true;
-    }
-  }
-  const float lim2 = (ANY || h.slot < 0) ? lim : h.t * 1.00001f;
-  float k[8];
-  int cnt = 0;
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    const bool in = ((hitm >> c) & 1u) && code[c] >= 0 && tn[c] <= lim2;
-    k[c] = in ? tn[c] : INFINITY;
-    cnt += in ? 1 : 0;
-  }
-  if (cnt > 0) {
-    cas8(k, code, 0, 2); cas8(k, code, 1, 3); cas8(k, code, 4, 6); cas8(k, code, 5, 7);
-    cas8(k, code, 0, 4); cas8(k, code, 1, 5); cas8(k, code, 2, 6); cas8(k, code, 3, 7);
-    cas8(k, code, 0, 1); cas8(k, code, 2, 3); cas8(k, code, 4, 5); cas8(k, code, 6, 7);
-    cas8(k, code, 2, 4); cas8(k, code, 3, 5);
-    cas8(k, code, 1, 4); cas8(k, code, 3, 6);
-    cas8(k, code, 1, 2); cas8(k, code, 3, 4); cas8(k, code, 5, 6);
-    if (sp + cnt - 1 > kStackDepth + kSpillDepth) {
-      *overflow = 1;
-    } else if (sp + cnt - 1 <= kStackDepth) {
-#pragma unroll
-      for (int j = 7; j > 0; j--)
-        if (j < cnt) stack[(sp++) * stride] = code[j];
-    } else if (kSpillDepth > 0) {
-#pragma unroll
-      for (int j = 7; j > 0; j--) {
-        if (j < cnt) {
-          if (sp < kStackDepth) stack[sp * stride] = code[j];
-          else spill[sp - kStackDepth] = code[j];
-          sp++;
-        }
-      }
-    }
-    node = code[0];
-    return false;
-  }
-  if (sp == 0) return true;
-  sp--;
-  node = (kSpillDepth == 0 || sp < kStackDepth) ? stack[sp * stride] : spill[sp - kStackDepth];
-  return false;
-}
-
 template <bool ANY>
 __device__ __forceinline__ bool traverse_step(const DevScene& S, const Ray& r, float tmin, float tmax, int* stack,
                                               int stride, int* spill, int& node, int& sp, HitInfo& h,
                                               int* overflow) {
-  if (kBvhWidth == 8) return traverse_step8<ANY>(S, r, tmin, tmax, stack, stride, spill, node, sp, h, overflow);
   return traverse_step4<ANY>(S, r, tmin, tmax, stack, stride, spill, node, sp, h, overflow);
 }
 

@@ -287,6 +287,11 @@ static void packet_visit(Packet* W, int t, int bucket) {
 // ONE queued key (production); policy 1: each lane merges ALL its queued keys.
 // Returns iterations; *rounds = insert rounds.
 static int QL = 8;
+// partial insert networks: per pop-one round, the wave's lowest insertion
+// position (entries below it are unchanged) rounded down to a checkpoint
+// multiple of NETCP; the network then runs from there (K - start entries)
+static int NETCP = 8;
+static double g_net_entries = 0, g_net_rounds = 0;
 typedef struct {
   const float* q; float cut, bound; List L; int prev, curr, depth, walking, qn; uint32_t far_mask; uint64_t qk[32];
 } Lane;
@@ -343,6 +348,19 @@ static int wave_lockstep(const float* const* qs, const float* cuts, int policy, 
             if (list_insert(&w->L, k)) { (*lane_ins)++; break; }
           }
         } else {
+          if (policy == 0 && l == 0) {   // the wave's lowest insertion position this round
+            int pmin = K;
+            for (int l2 = 0; l2 < 64; l2++) {
+              const Lane* u = &ln[l2];
+              if (u->qn <= 0) continue;
+              const uint64_t k = u->qk[u->qn - 1];
+              if (u->L.n >= K && !(k < u->L.key[K - 1])) continue;
+              int pos = 0;
+              while (pos < u->L.n && u->L.key[pos] < k) pos++;
+              if (pos < pmin) pmin = pos;
+            }
+            if (pmin < K) { g_net_entries += K - (pmin / NETCP) * NETCP; g_net_rounds++; }
+          }
           const int take = policy ? w->qn : (w->qn > 0);
           for (int t = 0; t < take; t++) {
             const uint64_t k = w->qk[--w->qn];
@@ -593,6 +611,7 @@ int main(int argc, char** argv) {
   const int sample = argc > 3 ? atoi(argv[3]) : 2000;
   if (argc > 4) BUCKET = atoi(argv[4]);
   if (argc > 5) QL = atoi(argv[5]);
+  if (getenv("NETCP")) NETCP = atoi(getenv("NETCP"));
   N = (int)np;
   T = malloc(sizeof(Node) * (size_t)N);
   int* v = malloc(sizeof(int) * (size_t)N);
@@ -1081,6 +1100,9 @@ int main(int argc, char** argv) {
     for (int v = 0; v < 3; v++)
       printf("P pooled 256 queries, refill at %d idle: iterations %.1f, rounds %.1f\n", refills[v], pit[v] / PS, prd[v] / PS);
   }
+  if (g_net_rounds > 0)
+    printf("partial networks (checkpoint %d): mean entries per round %.1f of %d (rounds with an insert %.0f)\n", NETCP,
+           g_net_entries / g_net_rounds, K, g_net_rounds);
   printf("seeded (triangle) cut / exact k-th d2: mean %.3f\n", s_ratio / s_n);
   for (int v = 0; v < 8; v++)
     printf("Y %s leader list kk=%d: cut/exact mean %.3f, iterations %.1f, rounds %.1f\n", v >> 2 ? "two" : "nearest",
