@@ -3,8 +3,8 @@
 csv: 5-ms windows, busy ms and the top kernels of each queue, and per-phase
 kernel overlap (which kernels ran beside which).
     python3 tools/timeline.py <..._kernel_trace.csv> [window_ms]
-The frame starts at the last photon-emission launch (k_ph_gen) of the global
-trace, i.e. the last frame's first kernel on the main queue."""
+The last frame spans from the first launch after the previous frame's
+k_resolve to its own k_resolve."""
 import collections
 import csv
 import re
@@ -26,13 +26,15 @@ def main():
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         ks.append((s, e, r.get("Queue_Id") or r.get("Stream_Id") or "?", short(r["Kernel_Name"])))
     ks.sort()
-    gens = [k for k in ks if k[3].startswith("k_ph_gen")]
-    if len(gens) < 2:
-        print("no k_ph_gen launches found")
+    # frames end with k_resolve; the last frame starts at the first launch
+    # after the previous frame's k_resolve
+    res = [k for k in ks if k[3].startswith("k_resolve")]
+    if len(res) < 2:
+        print("fewer than two frames (k_resolve launches) in the trace")
         return
-    # the last frame: from the first k_ph_gen of the last pair (global trace, then caustic)
-    t0 = gens[-2][0] if gens[-1][0] - gens[-2][0] < 20e6 else gens[-1][0]
-    frame = [k for k in ks if k[0] >= t0]
+    prev_end = res[-2][1]
+    frame = [k for k in ks if k[0] >= prev_end and k[0] <= res[-1][1]]
+    t0 = min(k[0] for k in frame)
     t1 = max(k[1] for k in frame)
     print(f"frame span {(t1 - t0) / 1e6:.1f} ms (first kernel start -> last kernel end); per HIP queue, "
           f"{win:g}-ms windows: busy ms, top kernels")
