@@ -604,22 +604,6 @@ constexpr int kGatherBox = PM_GATHER_BOX;
 #endif
 constexpr int kBoxAfter = PM_BOX_AFTER;
 
-#ifndef PM_GATHER_XCD
-#define PM_GATHER_XCD 0
-#endif
-#ifndef PM_GATHER_CHUNKS
-#define PM_GATHER_CHUNKS 1
-#endif
-#ifndef PM_GATHER_CHUNK_MIN
-#define PM_GATHER_CHUNK_MIN 1024   // leaders per chunk below which the gather runs unchunked
-#endif
-// bijective blockIdx remap: blocks b with equal b % 8 (one XCD, as the
-// dispatcher deals them) get consecutive logical ids (cdna_hip_programming T1)
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nwg) {
-  const uint32_t q = nwg / 8, r = nwg % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
 __device__ __forceinline__ double seed_bound(float4 lead, v3 q) {
   if (!(lead.w >= 0.f)) return 1e300;
   const double dx = (double)q.x - lead.x, dy = (double)q.y - lead.y, dz = (double)q.z - lead.z;
@@ -700,20 +684,15 @@ template <int TAG, bool LEADERS, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && (kGatherBox == 1 || kGatherBox == 2) ? 3 : 4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
-    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx, int64_t t0,
-    int64_t t1) {
-  // lanes [t0, t1) of the launch's kind (leader index / follower index): one
-  // chunk of the pipelined gather (launch_gather)
+    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx, int64_t t1) {
+  // lanes [0, t1): leader index (rank t S) or follower index
   __shared__ double lq[(kGatherQL + 1) * 256];
   const float R2 = kKMaxDistance * kKMaxDistance;
   // follower launch with a leader budget: the first nretry_blocks workgroups
   // (one lane per leader) re-walk the leaders that ran out of budget, with the
   // leaders' own cut-off; the walk and the epilogue are shared
   const int64_t nrb = (!LEADERS && nretry) ? (int64_t)retry_blocks : 0;
-  // XCD-aware block order (PM_GATHER_XCD): the blocks that share an XCD (b % 8)
-  // take one contiguous eighth of the walk order, so each XCD's L2 holds the
-  // tree neighbourhood of one compact query region instead of all eight
-  const uint32_t bid = PM_GATHER_XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t bid = blockIdx.x;
   const bool redo_lane = (int64_t)bid < nrb;
   int64_t r;
   bool valid;
@@ -722,7 +701,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
     valid = e < *nretry;
     r = valid ? (int64_t)retry[e] : 0;
   } else {
-    const int64_t t = t0 + ((int64_t)bid - nrb) * blockDim.x + threadIdx.x;
+    const int64_t t = ((int64_t)bid - nrb) * blockDim.x + threadIdx.x;
     r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
     valid = t < t1 && r < nq;
   }
@@ -861,9 +840,9 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
 #else
   const int64_t nl = (nq + kSeedStride - 1) / kSeedStride;   // leaders: walk ranks 0, S, 2S, ...
   DevBuf<float4> lead(nl);
-  DevBuf<uint32_t> retry(kLeaderBudget > 0 ? nl : 0), nretry(kLeaderBudget > 0 ? PM_GATHER_CHUNKS : 0);
+  DevBuf<uint32_t> retry(kLeaderBudget > 0 ? nl : 0), nretry(kLeaderBudget > 0 ? 1 : 0);
   if (!lead.p || (kLeaderBudget > 0 && (!retry.p || !nretry.p))) return hipErrorOutOfMemory;
-  if (kLeaderBudget > 0) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, sizeof(uint32_t) * PM_GATHER_CHUNKS, s));
+  if (kLeaderBudget > 0) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, sizeof(uint32_t), s));
   DevBuf<float4> box(kGatherBox ? 2 * (size_t)std::max<int64_t>(boxed_nodes(n, PM_GATHER_BOX_SKIP), 1) : 0);
   BoxView bx;
   hipEvent_t box_done = nullptr;
@@ -922,86 +901,32 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
     box_done = nullptr;
     return e;
   };
-  // Pipelined leaders (PM_GATHER_CHUNKS = C > 1): the walk order is cut into
-  // C chunks of whole leader strides; the leader launches run back to back on
-  // a side stream and follower chunk c (+ chunk c's retried leaders at its
-  // head) starts on s as soon as leader chunks c and c + 1 are done (its
-  // queries read the records of leaders jp - 1 .. jp + 2). The leader
-  // launches' last, under-filled rounds then overlap the followers of earlier
-  // chunks instead of idling the GPU before the first follower starts.
-  // C = 1: one leader launch, then one follower launch (rounds 1-3).
-  int C = PM_GATHER_CHUNKS;
-  // small gathers: chunks would under-fill the GPU; every chunk holds >= 2
-  // leaders, so follower chunk c's last records (jp + 2) lie in chunk c + 1
-  if (nl < (int64_t)C * std::max(PM_GATHER_CHUNK_MIN, 2)) C = 1;
-  hipStream_t ls = C > 1 ? side_stream(stream_device(s), 3) : nullptr;
-  if (C > 1 && !ls) C = 1;
-  std::vector<hipEvent_t> evs;
-  struct EvGuard {
-    std::vector<hipEvent_t>& v;
-    ~EvGuard() {
-      for (hipEvent_t e : v) (void)hipEventDestroy(e);
-    }
-  } ev_guard{evs};
-  for (int c = 0; C > 1 && c <= C; c++) {
-    hipEvent_t e = nullptr;
-    PM_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    evs.push_back(e);
-  }
-  if (C > 1) {   // the leader stream starts after everything before this call on s
-    PM_HIP_TRY(hipEventRecord(evs[C], s));
-    PM_HIP_TRY(hipStreamWaitEvent(ls, evs[C], 0));
-  }
-  auto lead_lo = [&](int c) -> int64_t { return nl * c / C; };
   const int64_t nf = nq - nl;
   // node byte offsets fit 32 bits below 2^28 nodes (saddr loads); larger maps use 64-bit addresses
   const bool wide = PM_FORCE_WIDE || n >= (1 << 28);
   uint32_t* const rt = kLeaderBudget > 0 ? retry.p : nullptr;
   uint32_t* const nrt = kLeaderBudget > 0 ? nretry.p : nullptr;
-  // one launch of k_gather_level<tag, LEADERS, wide> over lanes [t0, t1);
-  // chunk c's retry list is retry[lead_lo(c) ..], its count nretry[c]
-  auto level = [&](auto leaders, int c, int grid, int rb, int64_t t0, int64_t t1, hipStream_t st) -> hipError_t {
+  // one launch of k_gather_level<tag, LEADERS, wide> over lanes [0, t1)
+  auto level = [&](auto leaders, int grid, int rb, int64_t t1) -> hipError_t {
     constexpr bool L = decltype(leaders)::value;
     if (grid <= 0) return hipSuccess;
-    uint32_t* const cr = rt ? rt + lead_lo(c) : nullptr;
-    uint32_t* const cn = nrt ? nrt + c : nullptr;
     const float4 *nd = m->nodes.p, *pl = m->payload.p;
     if (tag == 1 && wide)
-      k_gather_level<1, L, true><<<grid, 256, 0, st>>>(nd, pl, n, qb, nq, out, perm, lead.p, cr, cn, rb, bx, t0, t1);
+      k_gather_level<1, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     else if (tag == 1)
-      k_gather_level<1, L, false><<<grid, 256, 0, st>>>(nd, pl, n, qb, nq, out, perm, lead.p, cr, cn, rb, bx, t0, t1);
+      k_gather_level<1, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     else if (wide)
-      k_gather_level<0, L, true><<<grid, 256, 0, st>>>(nd, pl, n, qb, nq, out, perm, lead.p, cr, cn, rb, bx, t0, t1);
+      k_gather_level<0, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     else
-      k_gather_level<0, L, false><<<grid, 256, 0, st>>>(nd, pl, n, qb, nq, out, perm, lead.p, cr, cn, rb, bx, t0, t1);
+      k_gather_level<0, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     return hipGetLastError();
   };
-  auto launch_leaders = [&](int c, hipStream_t st) -> hipError_t {
-    const int64_t a = lead_lo(c), b = lead_lo(c + 1);
-    return level(std::true_type{}, c, grid_for(b - a, 256), 0, a, b, st);
-  };
-  auto launch_followers = [&](int c) -> hipError_t {
-    const int64_t a = lead_lo(c), b = lead_lo(c + 1);
-    // follower index t <-> rank (t / (S - 1)) S + 1 + t % (S - 1): chunk c's ranks [a S, b S)
-    const int64_t f0 = std::min(a * (kSeedStride - 1), nf), f1 = c == C - 1 ? nf : std::min(b * (kSeedStride - 1), nf);
-    const int rb = kLeaderBudget > 0 ? grid_for(b - a, 256) : 0;   // chunk c's retried leaders: one lane each
-    return level(std::false_type{}, c, grid_for(f1 - f0, 256) + rb, rb, f0, f1, s);
-  };
-  if (C == 1) {
-    PM_HIP_TRY(launch_leaders(0, s));
-    PM_HIP_TRY(boxes_ready());
-    if (nf > 0 || kLeaderBudget > 0) PM_HIP_TRY(launch_followers(0));
-  } else {
-    for (int c = 0; c < C; c++) {
-      PM_HIP_TRY(launch_leaders(c, ls));
-      PM_HIP_TRY(hipEventRecord(evs[c], ls));
-    }
-    PM_HIP_TRY(boxes_ready());
-    for (int c = 0; c < C; c++) {
-      PM_HIP_TRY(hipStreamWaitEvent(s, evs[std::min(c + 1, C - 1)], 0));
-      PM_HIP_TRY(launch_followers(c));
-    }
-  }
+  // leaders (walk ranks 0, S, 2S, ...), then the followers with the retry
+  // workgroups first (one lane per leader, with a leader budget)
+  PM_HIP_TRY(level(std::true_type{}, grid_for(nl, 256), 0, nl));
+  PM_HIP_TRY(boxes_ready());
+  const int rb = kLeaderBudget > 0 ? grid_for(nl, 256) : 0;
+  if (nf > 0 || kLeaderBudget > 0) PM_HIP_TRY(level(std::false_type{}, grid_for(nf, 256) + rb, rb, nf));
   return hipGetLastError();
 #endif
 }
