@@ -1091,6 +1091,9 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, B
 // is its slowest wave's (config 5: 1,665 iterations per leader wave on
 // average, 4,557 at most); lanes still walking at the budget are redone at the
 // head of the follower launch, beside the followers.
+#ifndef PM_WIDE_RAD_CHUNK
+#define PM_WIDE_RAD_CHUNK 8   // keys per row read in the radiance sum (1: one 8-B load per key)
+#endif
 #ifndef PM_WIDE_LEADER_BUDGET
 #define PM_WIDE_LEADER_BUDGET 2048
 #endif
@@ -1226,6 +1229,30 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
       const bool full = cnt >= k;
       const float r2 = full ? gkey_d2(row[k - 1]) : R2;
       v3 flux = {0.f, 0.f, 0.f};
+#if PM_WIDE_RAD_CHUNK > 1
+      // the lane's sorted row read PM_WIDE_RAD_CHUNK keys at a time (16-B loads
+      // issued together: each row line is fetched once; one 8-B load per key
+      // re-fetched the 64 lanes' lines, which the wave's other rows evict)
+      for (int p0 = 0; p0 < m; p0 += PM_WIDE_RAD_CHUNK) {
+        double key[PM_WIDE_RAD_CHUNK];
+        const double2* src = reinterpret_cast<const double2*>(row + p0);
+#pragma unroll
+        for (int j = 0; j < PM_WIDE_RAD_CHUNK / 2; j++) {
+          const double2 d = src[j];
+          key[2 * j] = d.x;
+          key[2 * j + 1] = d.y;
+        }
+#pragma unroll
+        for (int j = 0; j < PM_WIDE_RAD_CHUNK; j++) {
+          if (p0 + j < m) {
+            const float4 pl = payload[gkey_word(key[j]) >> 2];
+            const float dist = sqrtf(gkey_d2(key[j]));
+            const float wgt = 1 - (dist / sqrtf(r2) * kConeFilterC);
+            flux = add(flux, smul(qq.w * pl.w * wgt, v3{pl.x, pl.y, pl.z}));
+          }
+        }
+      }
+#else
       for (int p = 0; p < m; p++) {
         const double key = row[p];
         const float4 pl = payload[gkey_word(key) >> 2];
@@ -1233,6 +1260,7 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
         const float wgt = 1 - (dist / sqrtf(r2) * kConeFilterC);
         flux = add(flux, smul(qq.w * pl.w * wgt, v3{pl.x, pl.y, pl.z}));
       }
+#endif
       const v3 f = divf(flux, (1 - (2.f / 3.f) * (1.f / kConeFilterC)) * 2 * kPI * r2);
       out[i] = make_float4(f.x, f.y, f.z, 0.f);
       if (LEADERS) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, full ? r2 : -1.f);
