@@ -1,5 +1,7 @@
 """kd-build time vs map size on one GPU (what every rank pays per frame at N GPUs
-under the replicated build): synthetic photons uniform in a box, N = k x 45.4M."""
+under the replicated build): synthetic photons uniform in a box, N = k x 45.4M.
+  KS="1 2 4 8" (map sizes), REPL=0 skips the replicated builds, SHARD=0 the
+  sharded ones, ROWS=0 the exchange's old compaction + re-expansion."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "photon-mapping_amd"))
@@ -7,7 +9,7 @@ import torch
 import pm_amd
 torch.cuda.set_device(0)
 base = 45_427_140
-for k in [int(x) for x in os.environ.get("KS", "1 2 4 8").split()]:
+for k in [int(x) for x in os.environ.get("KS", "1 2 4 8").split()] if os.environ.get("REPL", "1") == "1" else []:
     n = base * k
     g = torch.rand((n, 10), device="cuda", dtype=torch.float32) * 100.0
     c = torch.empty((0, 10), device="cuda", dtype=torch.float32)
