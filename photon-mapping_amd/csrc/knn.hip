@@ -956,6 +956,37 @@ constexpr int kWideMinK = 64;                         // k > this: collect and s
 
 __device__ __forceinline__ void fence_wave() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
+// Lane exchange v[lane ^ lj] without the LDS crossbar where the pattern allows:
+// xor 1 / 2 are DPP quad permutes, xor 4 = half_mirror then quad reverse, xor 8
+// = row_mirror then half_mirror (two DPP moves each), xor 16 a ds_swizzle; 32
+// stays a ds_bpermute. (Every __shfl_xor was a ds_bpermute: 970 of them in the
+// wide kernel, ~45 % of the final sorts' cost.)
+#ifndef PM_WIDE_DPP
+#define PM_WIDE_DPP 1
+#endif
+__device__ __forceinline__ int lane_xor(int v, int lj) {
+  if (!PM_WIDE_DPP) return __shfl_xor(v, lj);
+  switch (lj) {
+    case 1: return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1, 0, 3, 2]
+    case 2: return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2, 3, 0, 1]
+    case 4: {
+      const int w = __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);   // row_half_mirror: 7 - i in each 8
+      return __builtin_amdgcn_mov_dpp(w, 0x1B, 0xF, 0xF, false);           // quad_perm [3, 2, 1, 0]
+    }
+    case 8: {
+      const int w = __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);   // row_mirror: 15 - i in each 16
+      return __builtin_amdgcn_mov_dpp(w, 0x141, 0xF, 0xF, false);          // row_half_mirror
+    }
+    case 16: return __builtin_amdgcn_ds_swizzle(v, 0x1F | (16 << 10));   // bit mode, xor 16
+    default: return __shfl_xor(v, lj);
+  }
+}
+__device__ __forceinline__ double lane_xor(double v, int lj) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = lane_xor((int)(uint32_t)b, lj), hi = lane_xor((int)(uint32_t)(b >> 32), lj);
+  return __longlong_as_double((int64_t)((uint64_t)(uint32_t)hi << 32 | (uint32_t)lo));
+}
+
 // Bitonic sort (ascending) of 64 S keys held blocked: lane L holds elements
 // L S .. L S + S - 1. Strides >= S cross lanes (shuffles), smaller ones stay in
 // the lane's registers.
@@ -971,7 +1002,7 @@ __device__ __forceinline__ void wave_sort(double (&v)[S], int lane) {
         const bool keep_min = (((lane * S) & size) == 0) == ((lane & lj) == 0);
 #pragma unroll
         for (int r = 0; r < S; r++) {
-          const double p = __shfl_xor(v[r], lj);
+          const double p = lane_xor(v[r], lj);
           v[r] = keep_min ? dmin(v[r], p) : dmax(v[r], p);
         }
       } else {
