@@ -648,16 +648,23 @@ bool load_fbx(const std::string& path, RawScene& sc, std::string& err) {
   // model -> its geometries / materials / child models, in connection order
   std::map<int64_t, std::vector<int64_t>> mgeo, mmat, mkids;
   std::vector<int64_t> roots;
-  std::map<int64_t, int> nparents;
+  std::map<int64_t, int64_t> parent_of;
   for (const auto& [ch, par] : oo) {
     if (geoms.count(ch) && models.count(par)) mgeo[par].push_back(ch);
     else if (mats.count(ch) && models.count(par)) mmat[par].push_back(ch);
     else if (models.count(ch)) {
+      if (par != 0 && !models.count(par)) continue;
+      // a node hierarchy is a tree (as load_glb requires): one parent per
+      // model; the same child -> parent connection repeated is one edge
+      const auto it = parent_of.find(ch);
+      if (it != parent_of.end()) {
+        if (it->second == par) continue;
+        err = "FBX model " + std::to_string(ch) + " has two parents";
+        return false;
+      }
+      parent_of[ch] = par;
       if (par == 0) roots.push_back(ch);
-      else if (models.count(par)) mkids[par].push_back(ch);
-      else continue;
-      // a node hierarchy is a tree (as load_glb requires): one parent per model
-      if (++nparents[ch] > 1) { err = "FBX model " + std::to_string(ch) + " has two parents"; return false; }
+      else mkids[par].push_back(ch);
     }
   }
   static const char* complex[] = {"RotationOffset", "RotationPivot", "PreRotation", "PostRotation", "ScalingOffset",

@@ -961,6 +961,10 @@ __device__ __forceinline__ void fence_wave() { __builtin_amdgcn_fence(__ATOMIC_S
 // = row_mirror then half_mirror (two DPP moves each), xor 16 a ds_swizzle; 32
 // stays a ds_bpermute. (Every __shfl_xor was a ds_bpermute: 970 of them in the
 // wide kernel, ~45 % of the final sorts' cost.)
+// REQUIRES the whole wave active: the DPP moves use bound_ctrl = false, so a
+// source lane that is inactive yields an undefined value. wave_sort / row_sort
+// are called only from wave-uniform control flow; a caller under divergence
+// must use __shfl_xor instead.
 #ifndef PM_WIDE_DPP
 #define PM_WIDE_DPP 1
 #endif
@@ -1117,14 +1121,17 @@ __device__ __forceinline__ void collect_step(const float4* __restrict__ nodes, B
 }
 
 
+#ifndef PM_WIDE_RAD_CHUNK
+#define PM_WIDE_RAD_CHUNK 8   // keys per row read in the radiance sum (1: one 8-B load per key)
+#endif
+// the chunked read loads key pairs (16 B) and reads whole chunks of a row
+static_assert(PM_WIDE_RAD_CHUNK == 1 || (PM_WIDE_RAD_CHUNK % 2 == 0 && 64 % PM_WIDE_RAD_CHUNK == 0),
+              "PM_WIDE_RAD_CHUNK: 1 or an even divisor of 64 (rows hold 64 S keys)");
 // Leader step budget of the wide gather (wave iterations; 0: none): the
 // leader launch is a few thousand waves on an otherwise idle GPU, so its length
 // is its slowest wave's (config 5: 1,665 iterations per leader wave on
 // average, 4,557 at most); lanes still walking at the budget are redone at the
 // head of the follower launch, beside the followers.
-#ifndef PM_WIDE_RAD_CHUNK
-#define PM_WIDE_RAD_CHUNK 8   // keys per row read in the radiance sum (1: one 8-B load per key)
-#endif
 #ifndef PM_WIDE_LEADER_BUDGET
 #define PM_WIDE_LEADER_BUDGET 2048
 #endif
@@ -1144,6 +1151,7 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
                                                      uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry) {
   constexpr int CAP = 64 * S;
   static_assert(CAP % kChunkKeys == 0, "rows hold whole chunks");
+  static_assert(CAP % PM_WIDE_RAD_CHUNK == 0, "the radiance sum reads whole chunks of a row");
   const float R2 = kKMaxDistance * kKMaxDistance;
   const int lane = threadIdx.x & 63;
   double* const wrows = rows + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * CAP;

@@ -489,7 +489,9 @@ class PhotonRows:
     `segments` = [(first row, rows), ...] in map order."""
 
     def __init__(self, buf, segments, color_offset: int):
-        assert buf.dim() == 2 and buf.dtype.is_floating_point and buf.is_contiguous()
+        import torch
+        # the C side reads d_rows as float32 device rows (pm_photon_rows)
+        assert buf.dim() == 2 and buf.dtype == torch.float32 and buf.is_cuda and buf.is_contiguous()
         assert len(segments) <= ROWS_MAX_SEGS and 3 <= color_offset <= buf.shape[1] - 3
         assert all(0 <= r0 and 0 <= c and r0 + c <= buf.shape[0] for r0, c in segments)
         self.buf, self.segments, self.color_offset = buf, [(int(r0), int(c)) for r0, c in segments], int(color_offset)

@@ -557,8 +557,10 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
 def _gathered_set(x):
     """A finished photon all-gather as a map input: PhotonRows over the padded
     device buffer, or (host tensors: the CPU test backends) pm_photon rows."""
-    if x.out is not None:
+    if x.out is not None and x.world <= _pm().ROWS_MAX_SEGS:
         return x.rows()
+    # host tensors, or more ranks than pm_photon_rows has segments: the rows
+    # concatenated and re-expanded (a copy)
     return unpack_rows(x.wait())
 
 

@@ -474,6 +474,23 @@ def test_malformed_fbx_rejected(tmp_path, bad):
     assert e.value.status == pm_amd.PM_ERR_IO
 
 
+def test_fbx_repeated_parent_connection_is_one_edge(tmp_path):
+    """The same child -> parent OO connection listed twice is still a tree
+    (ADVICE r4): loaded as if listed once, not rejected as 'two parents'."""
+    objects = _fbx_node("Objects", [], [_geometry(11, "g", TRI.astype(np.float64), [[0, 1, 2]]),
+                                        _model(21, "m", **{"Lcl Translation": (5, 0, 0)}), _model(22, "k")])
+    C = lambda a, b: _fbx_node("C", ["OO", a, b])
+    once = [C(21, 0), C(22, 21), C(11, 22)]
+    out = {}
+    for name, conns in (("once", once), ("twice", once[:2] + [C(22, 21)] + once[2:])):
+        (tmp_path / f"{name}.fbx").write_bytes(_fbx_file([objects, _fbx_node("Connections", [], conns)]))
+        (tmp_path / "lights.txt").write_text("0 20 0 1 1 1 10\n")
+        out[name], _ = _load(str(tmp_path / f"{name}.fbx"))
+    assert len(out["twice"]) == len(out["once"]) == 1
+    assert np.array_equal(out["twice"][0].vertices, out["once"][0].vertices)
+    assert np.array_equal(out["once"][0].vertices, (TRI + [5, 0, 0]).astype(np.float32))
+
+
 def test_fbx_short_material_record_falls_back(tmp_path):
     """A Material record without its name property: the mesh takes
     DefaultMaterial instead of reading past the record."""
