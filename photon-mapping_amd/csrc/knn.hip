@@ -591,7 +591,7 @@ constexpr bool kLeaderSoft = PM_LEADER_SOFT;
 #define PM_GATHER_BOX 3
 #endif
 #ifndef PM_GATHER_BOX_SKIP
-#define PM_GATHER_BOX_SKIP 0
+#define PM_GATHER_BOX_SKIP 3
 #endif
 constexpr int kGatherBox = PM_GATHER_BOX;
 // 1 (test variant): 64-bit node addressing for every map, so the path that
@@ -1051,7 +1051,7 @@ __device__ __forceinline__ double row_sort(double* __restrict__ row, int cnt, in
 #define PM_WIDE_BOX 1   // 0: plane test only (A/B variants)
 #endif
 #ifndef PM_WIDE_BOX_SKIP
-#define PM_WIDE_BOX_SKIP 0   // boxes down to level D - skip (0: every node)
+#define PM_WIDE_BOX_SKIP 3   // boxes down to level D - skip (0: every node)
 #endif
 
 // One collect step of every lane: lean_step's walk and point test (with the

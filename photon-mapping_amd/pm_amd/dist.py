@@ -154,6 +154,24 @@ class _PhaseClock:
         return self.a.elapsed_time(self.b) * 1e3
 
 
+class _HostStagedWork:
+    """A host-staged collective in flight: wait() waits for gloo, then copies
+    the host result into the caller's (device) tensor, once."""
+
+    def __init__(self, work, host, out):
+        self.work, self.host, self.out = work, host, out
+
+    def is_completed(self) -> bool:
+        return self.work is None or self.work.is_completed()
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.out.copy_(self.host)
+            self.work = self.host = None
+        return True
+
+
 class HostStagedDist:
     """torch.distributed over gloo with CUDA tensors staged through host memory:
     lets several ranks share one GPU (tests, and `bench.py` with
@@ -171,10 +189,17 @@ class HostStagedDist:
             o.copy_(h)
 
     def all_gather_into_tensor(self, out, t, async_op=False):
+        """async_op: gloo runs the all-gather on its worker thread and the
+        returned handle's wait() finishes it (then stages the result into
+        `out`), so the caller's work between start and wait overlaps it, as
+        with RCCL's stream (dist._maps: the caustic map and the distributed top
+        selection's all-reduces run while the global photons are in flight)."""
         h = self.t.empty_like(out, device="cpu")
-        self.d.all_gather_into_tensor(h, t.cpu())
-        out.copy_(h)
-        return None   # completed (host-staged): nothing to wait for
+        pending = _HostStagedWork(self.d.all_gather_into_tensor(h, t.cpu(), async_op=True), h, out)
+        if async_op:
+            return pending
+        pending.wait()
+        return None
 
     def reduce(self, t, dst, op):
         h = t.cpu()

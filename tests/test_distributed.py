@@ -186,3 +186,49 @@ def test_pack_rows_round_trip():
     u = unpack_rows(pack_rows(t))
     keep = [0, 1, 2, 7, 8, 9]
     assert torch.equal(u[:, keep], t[:, keep]) and torch.count_nonzero(u[:, 3:7]) == 0
+
+
+def _async_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pm_amd.dist import HostStagedDist
+        hd = HostStagedDist(dist)
+        t = torch.full((3, 2), float(rank + 1))
+        out = torch.zeros((3 * world, 2))
+        work = hd.all_gather_into_tensor(out, t, async_op=True)
+        assert work is not None
+        # collectives issued while the all-gather is pending (dist._maps: the
+        # top selection's all-reduces) complete in order on every rank
+        s = torch.tensor([rank + 1.0])
+        hd.all_reduce(s, dist.ReduceOp.SUM)
+        work.wait()
+        work.wait()   # idempotent
+        out2 = torch.zeros((3 * world, 2))
+        assert hd.all_gather_into_tensor(out2, t) is None   # synchronous form
+        q.put((rank, out.numpy().copy(), float(s.item()), torch.equal(out, out2)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_staged_all_gather_is_async():
+    """HostStagedDist.all_gather_into_tensor(async_op=True) returns a pending
+    handle: the result lands in `out` at wait(), and
+    collectives issued in between still match across ranks."""
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_async_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (o, s, same)) for r, o, s, same in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = np.concatenate([np.full((3, 2), r + 1.0, np.float32) for r in range(world)])
+    for r in range(world):
+        o, s, same = res[r]
+        assert np.array_equal(o, want) and s == 3.0 and same

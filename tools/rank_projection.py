@@ -8,7 +8,8 @@ slowest rank's phases, and a projection that puts back what one GPU cannot
 measure: the RCCL all-gathers over xGMI at an assumed receive bandwidth.
 
   WORLDS="2 4 8"  CONFIG=3|5  XGMI_GBS="300 450"  (effective all-gather receive
-  bandwidth per GPU, GB/s; MI355X: 7 xGMI links per GPU)"""
+  bandwidth per GPU, GB/s; MI355X: 7 xGMI links per GPU)  RANKS="0 2" (ranks to
+  run; default all)  REPS=2 (frames per rank, the last is reported)"""
 import json
 import os
 import sys
@@ -41,13 +42,15 @@ for world in [int(x) for x in os.environ.get("WORLDS", "2 4 8").split()]:
     emitted = sum(pm_amd.compute_photons_per_watt(lights, cfg.casted)) + \
         sum(pm_amd.compute_photons_per_watt(lights, cfg.caustic))
     ranks = []
-    for r in range(world):
-        for rep in range(2):   # the first frame of a rank pays its allocations
+    sel = [int(x) for x in os.environ["RANKS"].split()] if os.environ.get("RANKS") else range(world)
+    for r in [r for r in sel if r < world]:
+        for rep in range(int(os.environ.get("REPS", "2"))):   # the first frame of a rank pays its allocations
             _, info, ms = replay.rank_frame(rec, scene, lights, cfg, r)
         ranks.append((ms, {k: round(v / 1e3, 2) for k, v in info["us"].items()}))
         print(f"# N={world} rank {r}: {ms:.1f} ms {ranks[-1][1]}", file=sys.stderr, flush=True)
-    slow = max(range(world), key=lambda r: ranks[r][0])
+    slow = max(range(len(ranks)), key=lambda r: ranks[r][0])
     ms, ph = ranks[slow]
+    slow = list(sel)[slow]
     tags_bytes = (world - 1) / world * sum(rec.plan_sizes) * 4
     proj = {}
     for bw in bws:
