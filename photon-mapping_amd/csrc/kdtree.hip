@@ -635,6 +635,59 @@ __device__ __forceinline__ void block_bitonic(uint64_t& k, int& v, int n2, uint6
   }
 }
 
+// The three lists' sorts as ONE network (PM_KD_SORT3): every thread carries its
+// element's three (key, slot) pairs through the same compare-exchange stages,
+// so the stages that exchange through LDS pay their two block barriers once
+// for all three lists instead of once per list (30 instead of 90 barriers per
+// 1024-element block), and each in-wave stage has three independent chains.
+// kx / vx: 3 kLocal u64 and 3 kLocal i16 of LDS scratch.
+#ifndef PM_KD_SORT3
+#define PM_KD_SORT3 1
+#endif
+__device__ __forceinline__ void block_bitonic3(uint64_t (&k)[3], int (&v)[3], int n2, uint64_t* kx, int16_t* vx) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int ls = 1; ls <= 10; ls++) {
+    const int size = 1 << ls;
+#pragma unroll
+    for (int lst = ls - 1; lst >= 0; lst--) {
+      if (size > n2) continue;   // uniform
+      const int stride = 1 << lst;
+      uint64_t pk[3];
+      int pv[3];
+      if (stride >= 64) {
+        __syncthreads();
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+          kx[d * kLocal + tid] = k[d];
+          vx[d * kLocal + tid] = (int16_t)v[d];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+          pk[d] = kx[d * kLocal + (tid ^ stride)];
+          pv[d] = vx[d * kLocal + (tid ^ stride)];
+        }
+      } else {
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+          pk[d] = (uint64_t)(uint32_t)xor_lane((int)(uint32_t)k[d], stride) |
+                  (uint64_t)(uint32_t)xor_lane((int)(uint32_t)(k[d] >> 32), stride) << 32;
+          pv[d] = xor_lane(v[d], stride);
+        }
+      }
+      const bool up = (tid & size) == 0, lower = (tid & stride) == 0;
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        if (lower == up ? pk[d] < k[d] : pk[d] > k[d]) {
+          k[d] = pk[d];
+          v[d] = pv[d];
+        }
+      }
+    }
+  }
+}
+
 // SORT (the selection build): the subtree's elements arrive unsorted in E; the
 // three lists are made in LDS by sorting (orderable coordinate, index) keys,
 // the presort's order. Otherwise they are loaded from the presorted lists.
@@ -665,16 +718,47 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     }
     int n2 = 64;
     while (n2 < S) n2 <<= 1;
-    uint64_t* kx = reinterpret_cast<uint64_t*>(stage);   // scratch until stage is set below
-#pragma unroll 1
-    for (int d = 0; d < 3; d++) {
-      uint64_t k = tid < S ? (uint64_t)orderable_key(coord_of(me, d)) << 32 | (uint32_t)__float_as_int(me.w) : ~0ull;
-      int v = tid;
-      block_bitonic(k, v, n2, kx, tag);
+    if (PM_KD_SORT3) {
+      // scratch: buf[0] and buf[1] (written only after the sort), 24 KB of keys
+      // then 6 KB of slots
+      uint64_t* kx = reinterpret_cast<uint64_t*>(&buf[0][0]);
+      int16_t* vx = reinterpret_cast<int16_t*>(kx + 3 * kLocal);
+      uint64_t k[3];
+      int v[3];
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        k[d] = tid < S ? (uint64_t)orderable_key(coord_of(me, d)) << 32 | (uint32_t)__float_as_int(me.w) : ~0ull;
+        v[d] = tid;
+      }
+      block_bitonic3(k, v, n2, kx, vx);
       __syncthreads();   // buf[2] written; every exchange read
-      const float4 x = tid < S ? buf[2][v] : me;
-      if (d == 2) __syncthreads();
-      if (tid < S) buf[d][tid] = x;
+      // (loads only under tid < S: a select between an LDS element and a
+      // register value compiled to a flat load through scratch)
+      float4 x0, x1, x2;
+      if (tid < S) {
+        x0 = buf[2][v[0]];
+        x1 = buf[2][v[1]];
+        x2 = buf[2][v[2]];
+      }
+      __syncthreads();
+      if (tid < S) {
+        buf[0][tid] = x0;
+        buf[1][tid] = x1;
+        buf[2][tid] = x2;
+      }
+    } else {
+      uint64_t* kx = reinterpret_cast<uint64_t*>(stage);   // scratch until stage is set below
+#pragma unroll 1
+      for (int d = 0; d < 3; d++) {
+        uint64_t k = tid < S ? (uint64_t)orderable_key(coord_of(me, d)) << 32 | (uint32_t)__float_as_int(me.w) : ~0ull;
+        int v = tid;
+        block_bitonic(k, v, n2, kx, tag);
+        __syncthreads();   // buf[2] written; every exchange read
+        float4 x;
+        if (tid < S) x = buf[2][v];
+        if (d == 2) __syncthreads();
+        if (tid < S) buf[d][tid] = x;
+      }
     }
     __syncthreads();
   } else {
@@ -788,7 +872,11 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     int dim = 0;
     if (ext[1] > ext[dim]) dim = 1;
     if (ext[2] > ext[dim]) dim = 2;
-    const float4 sel = dim == 0 ? e[0] : (dim == 1 ? e[1] : e[2]);
+    // per component: a select of whole float4s indexed e[] dynamically,
+    // which kept e[] in scratch for the whole wave phase
+    const bool d0 = dim == 0, d1 = dim == 1;
+    const float4 sel = make_float4(d0 ? e[0].x : (d1 ? e[1].x : e[2].x), d0 ? e[0].y : (d1 ? e[1].y : e[2].y),
+                                   d0 ? e[0].z : (d1 ? e[1].z : e[2].z), d0 ? e[0].w : (d1 ? e[1].w : e[2].w));
     const int lm = placed ? lane : b + ls - b0;
     const float4 m = make_float4(__shfl(sel.x, lm), __shfl(sel.y, lm), __shfl(sel.z, lm), __shfl(sel.w, lm));
     const int nid = __float_as_int(m.w);
