@@ -58,9 +58,13 @@ def host_cores():
     return use, nproc, aff, quota
 
 
-def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
+def cpu_baseline(meshes, lights, args, n_global_full, nthreads, full_photons=None):
     """Scalar oracle (oracle/libpm_oracle.so, pthreads) on a bounded sample of the
-    same workload, scaled linearly to one frame."""
+    same workload, scaled linearly to one frame. full_photons = (diffuse,
+    caustic) pm_photon arrays of the whole frame (the GPU trace's, bitwise the
+    oracle's: tests/test_gpu_fullsize.py): the maps are then built from all of
+    them (timed, not scaled) and the sampled rows are rendered over maps of the
+    frame's own photon density; without them, maps of the traced sample."""
     import numpy as np
     import oracle
     t0 = time.time()
@@ -75,6 +79,8 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
     g = oracle.trace(sc, lights, args.casted, args.max_depth, False, nthreads=nthreads, g_range=(0, sg))
     c = oracle.trace(sc, lights, args.caustic, args.max_depth, True, nthreads=nthreads, g_range=(0, scn))
     t_trace = (time.time() - t) / frac
+    if full_photons is not None:
+        g, c = full_photons
     t = time.time()
     gm = oracle.PhotonMap(g, 1.0, c, 0.5, nthreads=nthreads)
     cm = oracle.PhotonMap(c, 0.5, nthreads=nthreads)
@@ -95,9 +101,14 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads):
         "value": P / total / 1e6, "unit": "Mphotons/s", "cores": nthreads, "kind": "port",
         "nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
         "sample": (f"oracle (pthreads x{nthreads}) traced {sg + scn} of {P} photons (scaled x{1 / frac:.1f}), "
-                   f"kd-built {n_s} photons (scaled N log N to {n_global_full}), rendered {rows} of "
-                   f"{args.height} rows at {args.width} px (scaled x{args.height / rows:.1f}) with the sampled "
-                   f"maps; wall {time.time() - t0:.1f}s"),
+                   + (f"kd-built the frame's full maps ({n_s} photons, the GPU trace's photons, bitwise the "
+                      f"oracle's), rendered {rows} of {args.height} rows at {args.width} px (scaled "
+                      f"x{args.height / rows:.1f}) over those full-density maps"
+                      if full_photons is not None and n_s == n_global_full else
+                      f"kd-built {n_s} photons (scaled N log N to {n_global_full}), rendered {rows} of "
+                      f"{args.height} rows at {args.width} px (scaled x{args.height / rows:.1f}) over maps of the "
+                      f"traced sample ({n_global_full / n_s:.1f}x sparser than the frame's)")
+                   + f"; wall {time.time() - t0:.1f}s"),
         "ms_per_frame": total * 1e3,
         "phase_s": {"trace": t_trace, "build": t_build, "render": t_render},
     }
@@ -187,6 +198,8 @@ def main():
                     help="CPU-baseline threads (0: every CPU this process may use, see host_cores)")
     ap.add_argument("--cpu-sample-photons", type=int, default=2_000_000)
     ap.add_argument("--cpu-sample-rows", type=int, default=48)
+    ap.add_argument("--cpu-sample-maps", action="store_true",
+                    help="CPU baseline maps from its traced sample (sparser) instead of the frame's photons")
     args = ap.parse_args()
     c2 = args.config == 2
     if args.scene is None:
@@ -353,8 +366,15 @@ def main():
     if rank == 0 and world == 1 and args.config == 3 and not args.no_secondary:
         out["secondary"] = {"config2": secondary_config2(args)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the frame's photons (traced again after the timed region, on the GPU)
+        # for the baseline's maps: its render leg walks maps of the frame's density
+        full = None
+        if not args.cpu_sample_maps:
+            gp = pm_amd.run_point_light_ray_gen(scene, lights, casted_total, args.max_depth, False, out=gbuf)
+            cp = pm_amd.run_point_light_ray_gen(scene, lights, caustic_total, args.max_depth, True, out=cbuf)
+            full = (gp.cpu().numpy(), cp.cpu().numpy())
         out["cpu_baseline"] = cpu_baseline(meshes, lights, args, info["n_global"],
-                                           args.cpu_threads or host_cores()[0])
+                                           args.cpu_threads or host_cores()[0], full_photons=full)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -800,10 +800,18 @@ void orc_map_destroy(orc_map* m) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* cukd::buildTree<Photon, Photon_traits> layout (ray-tracer/src/hostCode.cu:
- * 94-95; traits ray-tracer/include/photon.h:23-40, has_explicit_dim), restated
- * as the build rules DESIGN.md §4.3 fixes (cudaKDTree is an empty submodule in
- * the reference, so its published rules are what is restated):
+/* The left-balanced layout of cukd::buildTree<Photon, Photon_traits>
+ * (ray-tracer/src/hostCode.cu:94-95; traits ray-tracer/include/photon.h:23-40,
+ * has_explicit_dim), as THIS BUILD SPECIFIES it: the layout
+ * tests are spec-pinned, cukd-unpinned. cudaKDTree is an empty submodule in
+ * the reference, and two of the rules below are this build's own choices:
+ *   - the split dimension comes from the extent of the subtree's own POINTS;
+ *     cudaKDTree's explicit-dim builders may take it from the node's domain
+ *     box instead (the world bounds, which the reference passes as
+ *     globalPhotonsBounds, clipped at every ancestor's split plane);
+ *   - ties between equal coordinates break by original index (the
+ *     reference's thrust sort leaves their order unspecified).
+ * The rules:
  *   - the tree is the implicit complete binary tree, children 2t+1 / 2t+2, over
  *     the n records in place; subtree t holds s elements, its root the element
  *     of rank left_size(s) (complete-tree left subtree size), the left child the

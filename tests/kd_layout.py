@@ -1,7 +1,10 @@
-"""The kd-tree layout expected from the oracle (oracle.kd_left_balanced, the
-restatement of cukd::buildTree's in-place left-balanced tree,
-ray-tracer/src/hostCode.cu:94-95): the records a HIP build must produce, node
-for node, so the GPU tests can compare them bit for bit.
+"""The kd-tree layout expected from the oracle (oracle.kd_left_balanced: the
+in-place left-balanced tree of cukd::buildTree, ray-tracer/src/hostCode.cu:
+94-95, as this build specifies it): the records a HIP build must produce, node
+for node, so the GPU tests can compare them bit for bit. SPEC-PINNED,
+CUKD-UNPINNED: the split dimension from the subtree's point extent and the
+tie order by original index are this build's rules (oracle/pm_oracle.c, the
+layout header); cudaKDTree itself is absent.
   - map_records: pm_photon_map_export's output for a map built from photon
     sets (loadPhotons order, ray-tracer/src/hostCode.cu:54-99: a ++ b, their
     powers); a NaN coordinate is stored as +inf (include/pm.h), dir is zero;
