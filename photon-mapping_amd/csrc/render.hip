@@ -423,11 +423,57 @@ __global__ void k_compact_q(const float4* q, const uint32_t* valid, const uint32
 }
 
 // 30-bit Morton code of each query position (scene bounds) + identity permutation
+// Query walk order (PM_QUERY_ORDER): 0 Morton, 1 Hilbert. A 30-bit 3-D Hilbert
+// key (Skilling, "Programming the Hilbert curve", AIP Conf. Proc. 707, 2004:
+// axes to transpose, then the transpose's bits interleaved) never jumps between
+// distant cells the way Morton order does at its power-of-two seams, so the 64
+// queries of a wave and a follower's leaders lie closer together.
+#ifndef PM_QUERY_ORDER
+#define PM_QUERY_ORDER 1
+#endif
+__device__ __forceinline__ uint32_t hilbert30(float x, float y, float z, float3 lo, float3 inv) {
+  uint32_t X0 = (uint32_t)fminf(fmaxf((x - lo.x) * inv.x * 1024.0f, 0.0f), 1023.0f);
+  uint32_t X1 = (uint32_t)fminf(fmaxf((y - lo.y) * inv.y * 1024.0f, 0.0f), 1023.0f);
+  uint32_t X2 = (uint32_t)fminf(fmaxf((z - lo.z) * inv.z * 1024.0f, 0.0f), 1023.0f);
+  // inverse undo (every loop has constant bounds: the coordinates stay in registers)
+#pragma unroll
+  for (uint32_t Q = 1u << 9; Q > 1; Q >>= 1) {
+    const uint32_t P = Q - 1;
+    // i = 0: X0 & Q ? invert X0 : exchange X0 with itself (a no-op)
+    if (X0 & Q) X0 ^= P;
+    if (X1 & Q) {
+      X0 ^= P;
+    } else {
+      const uint32_t t = (X0 ^ X1) & P;
+      X0 ^= t;
+      X1 ^= t;
+    }
+    if (X2 & Q) {
+      X0 ^= P;
+    } else {
+      const uint32_t t = (X0 ^ X2) & P;
+      X0 ^= t;
+      X2 ^= t;
+    }
+  }
+  // Gray encode
+  X1 ^= X0;
+  X2 ^= X1;
+  uint32_t t = 0;
+#pragma unroll
+  for (uint32_t Q = 1u << 9; Q > 1; Q >>= 1)
+    if (X2 & Q) t ^= Q - 1;
+  X0 ^= t;
+  X1 ^= t;
+  X2 ^= t;
+  return (spread3(X0) << 2) | (spread3(X1) << 1) | spread3(X2);
+}
+
 __global__ void k_query_morton(const float4* q, int64_t n, float3 lo, float3 inv, uint32_t* keys, uint32_t* perm) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float4 p = q[i];
-  keys[i] = morton30(p.x, p.y, p.z, lo, inv);
+  keys[i] = PM_QUERY_ORDER == 1 ? hilbert30(p.x, p.y, p.z, lo, inv) : morton30(p.x, p.y, p.z, lo, inv);
   perm[i] = (uint32_t)i;
 }
 // Gathers run in Morton order of the query points (a pure permutation:
