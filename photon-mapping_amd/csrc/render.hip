@@ -423,21 +423,30 @@ __global__ void k_compact_q(const float4* q, const uint32_t* valid, const uint32
 }
 
 // 30-bit Morton code of each query position (scene bounds) + identity permutation
-// Query walk order (PM_QUERY_ORDER): 0 Morton, 1 Hilbert. A 30-bit 3-D Hilbert
-// key (Skilling, "Programming the Hilbert curve", AIP Conf. Proc. 707, 2004:
-// axes to transpose, then the transpose's bits interleaved) never jumps between
+// Query walk order (PM_QUERY_ORDER): 0 Morton, 1 Hilbert. A 3-D Hilbert key
+// (Skilling, "Programming the Hilbert curve", AIP Conf. Proc. 707, 2004: axes
+// to transpose, then the transpose's bits interleaved) never jumps between
 // distant cells the way Morton order does at its power-of-two seams, so the 64
 // queries of a wave and a follower's leaders lie closer together.
+// PM_QUERY_BITS per axis (3 x bits of key: the radix sort runs ceil(3 bits / 8)
+// passes); queries sharing a cell keep their dense (pixel, sample) order.
 #ifndef PM_QUERY_ORDER
 #define PM_QUERY_ORDER 1
 #endif
-__device__ __forceinline__ uint32_t hilbert30(float x, float y, float z, float3 lo, float3 inv) {
-  uint32_t X0 = (uint32_t)fminf(fmaxf((x - lo.x) * inv.x * 1024.0f, 0.0f), 1023.0f);
-  uint32_t X1 = (uint32_t)fminf(fmaxf((y - lo.y) * inv.y * 1024.0f, 0.0f), 1023.0f);
-  uint32_t X2 = (uint32_t)fminf(fmaxf((z - lo.z) * inv.z * 1024.0f, 0.0f), 1023.0f);
+#ifndef PM_QUERY_BITS
+#define PM_QUERY_BITS 10
+#endif
+constexpr int kQueryBits = PM_QUERY_BITS;
+static_assert(kQueryBits >= 1 && kQueryBits <= 10, "3 x PM_QUERY_BITS must fit the 30-bit spread");
+__device__ __forceinline__ uint32_t query_cell(float c, float lo, float inv) {
+  constexpr float cells = (float)(1u << kQueryBits);
+  return (uint32_t)fminf(fmaxf((c - lo) * inv * cells, 0.0f), cells - 1.0f);
+}
+__device__ __forceinline__ uint32_t hilbert_key(float x, float y, float z, float3 lo, float3 inv) {
+  uint32_t X0 = query_cell(x, lo.x, inv.x), X1 = query_cell(y, lo.y, inv.y), X2 = query_cell(z, lo.z, inv.z);
   // inverse undo (every loop has constant bounds: the coordinates stay in registers)
 #pragma unroll
-  for (uint32_t Q = 1u << 9; Q > 1; Q >>= 1) {
+  for (uint32_t Q = 1u << (kQueryBits - 1); Q > 1; Q >>= 1) {
     const uint32_t P = Q - 1;
     // i = 0: X0 & Q ? invert X0 : exchange X0 with itself (a no-op)
     if (X0 & Q) X0 ^= P;
@@ -461,19 +470,23 @@ __device__ __forceinline__ uint32_t hilbert30(float x, float y, float z, float3 
   X2 ^= X1;
   uint32_t t = 0;
 #pragma unroll
-  for (uint32_t Q = 1u << 9; Q > 1; Q >>= 1)
+  for (uint32_t Q = 1u << (kQueryBits - 1); Q > 1; Q >>= 1)
     if (X2 & Q) t ^= Q - 1;
   X0 ^= t;
   X1 ^= t;
   X2 ^= t;
   return (spread3(X0) << 2) | (spread3(X1) << 1) | spread3(X2);
 }
+__device__ __forceinline__ uint32_t morton_key(float x, float y, float z, float3 lo, float3 inv) {
+  return (spread3(query_cell(x, lo.x, inv.x)) << 2) | (spread3(query_cell(y, lo.y, inv.y)) << 1) |
+         spread3(query_cell(z, lo.z, inv.z));
+}
 
 __global__ void k_query_morton(const float4* q, int64_t n, float3 lo, float3 inv, uint32_t* keys, uint32_t* perm) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float4 p = q[i];
-  keys[i] = PM_QUERY_ORDER == 1 ? hilbert30(p.x, p.y, p.z, lo, inv) : morton30(p.x, p.y, p.z, lo, inv);
+  keys[i] = PM_QUERY_ORDER == 1 ? hilbert_key(p.x, p.y, p.z, lo, inv) : morton_key(p.x, p.y, p.z, lo, inv);
   perm[i] = (uint32_t)i;
 }
 // Gathers run in Morton order of the query points (a pure permutation:
@@ -498,7 +511,7 @@ static hipError_t sort_queries(const float4* dense, int64_t n, const pm_box& bb,
   const float3 inv = make_float3(ex > 0.f ? 1.0f / ex : 0.f, ey > 0.f ? 1.0f / ey : 0.f, ez > 0.f ? 1.0f / ez : 0.f);
   k_query_morton<<<grid_for(n, 256), 256, 0, s>>>(dense, n, lo, inv, Q.keys.p, Q.perm.p);
   PM_HIP_TRY(hipGetLastError());
-  return radix_sort_pairs(Q.keys.p, Q.perm.p, n, 30, s);
+  return radix_sort_pairs(Q.keys.p, Q.perm.p, n, 3 * kQueryBits, s);
 }
 
 static hipError_t gather_sorted(const pm_photon_map* m, SortedQueries& Q, float4* res, int tag, hipStream_t s,
