@@ -254,6 +254,9 @@ int pm_kd_shard_plan_create(const pm_photon* d_a, int64_t na, float power_a,
                             int32_t world, pm_kd_shard_plan** out, void* stream);
 /* *count = number of subtrees (2^L or 0); h_sizes (count entries) may be NULL. */
 int pm_kd_shard_subtrees(const pm_kd_shard_plan* plan, int32_t* count, int64_t* h_sizes);
+/* Builds of different subtrees of one plan may run at the same time from
+ * several host threads, each on its own stream (the rank's subtrees side by
+ * side); the call returns when its stream is done. */
 int pm_kd_shard_build(pm_kd_shard_plan* plan, int32_t subtree, int32_t* d_tags /* size */,
                       void* stream);
 /* d_tags: all subtrees' tags in subtree order (NULL if count == 0). */

@@ -558,6 +558,7 @@ struct pm_kd_shard_plan {
   DevBuf<float4> elems, payload, top;
   DevBuf<uint8_t> sub;   // subtree of every element (255: a top node)
   DevBuf<uint32_t> boff;  // per-tile subtree starts (kd_shard_offsets), made by the first build
+  std::mutex boff_mu;     // builds of one plan may run from several host threads (streams) at once
   int64_t n = 0;
   int L = 0;   // 0: not split
   std::vector<int64_t> sizes;
@@ -645,10 +646,17 @@ int pm_kd_shard_build(pm_kd_shard_plan* p, int32_t j, int32_t* d_tags, void* str
   {
     PhaseTimer tm(PH_KDBUILD, s);
     e = hipSuccess;
-    if (!p->boff.p) {
-      p->boff.alloc((size_t)kd_shard_tiles(p->n) * p->sizes.size());
-      e = p->boff.p ? kd_shard_offsets(p->sub.p, p->n, (int)p->sizes.size(), p->sizes.data(), p->boff.p, s) : hipErrorOutOfMemory;
-      if (e != hipSuccess) p->boff.reset();
+    {
+      // the offsets are made once, by the first build (kd_shard_offsets
+      // synchronises its stream, so a build on another stream may use them
+      // as soon as the lock is released)
+      std::lock_guard<std::mutex> lk(p->boff_mu);
+      if (!p->boff.p) {
+        p->boff.alloc((size_t)kd_shard_tiles(p->n) * p->sizes.size());
+        e = p->boff.p ? kd_shard_offsets(p->sub.p, p->n, (int)p->sizes.size(), p->sizes.data(), p->boff.p, s)
+                      : hipErrorOutOfMemory;
+        if (e != hipSuccess) p->boff.reset();
+      }
     }
     if (e == hipSuccess) e = kd_shard_subtree(p->elems.p, p->sub.p, p->boff.p, p->n, j, p->sizes[j], d_tags, s);
   }
