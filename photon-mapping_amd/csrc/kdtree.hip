@@ -539,7 +539,7 @@ __global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void 
 }
 
 // ------------------------------------------------------------------ local finish
-// Once every segment holds <= kLocal - 1 elements (global level L0 = H - 10),
+// Once every segment holds <= kLocal - 1 elements (global level L0 = H - kLocalLog),
 // one workgroup per segment finishes all remaining levels in LDS: the three
 // presorted lists of its range are loaded once (48 KB), and each local level
 // picks every sub-segment's widest dimension and median from the lists,
@@ -547,12 +547,24 @@ __global__ __launch_bounds__(kPartThreads) PM_WAVES_ATTR(PM_KD_PART_WAVES) void 
 // place (every thread holds its three elements in registers across the
 // barrier). Same rules as the global levels, so the tree is identical; the
 // bottom ~10 levels no longer cost a global read + write each.
-constexpr int kLocal = 1024;
-// From local level 4 on every sub-segment has <= 63 elements and there are 16 of
-// them: sub-segment j is finished by wave j with shuffles, a packed wave scan
-// and ds_permute (no block barriers, no LDS); same rules, same tree.
-constexpr int kLocalWaveLevel = 4;
-static_assert(kLocal / 64 == (1 << kLocalWaveLevel), "one wave per level-4 sub-segment");
+// PM_KD_LOCAL_LOG: log2 of the workgroup (10: 1024 threads, subtrees of <= 1023
+// elements, two workgroups per CU; 9: 512 threads, one more global level, four
+// workgroups per CU -- 32 waves either way -- with barriers half as wide and
+// 45 instead of 55 sort stages). Measured on config 3: the kd phase 24.0 ms
+// with 10, 31.2-31.7 ms with 9 (the extra global level costs more than the
+// narrower finish saves); the tree is the same (parity tests pass with both).
+#ifndef PM_KD_LOCAL_LOG
+#define PM_KD_LOCAL_LOG 10
+#endif
+constexpr int kLocalLog = PM_KD_LOCAL_LOG;
+constexpr int kLocal = 1 << kLocalLog;
+// From local level kLocalLog - 6 on every sub-segment has <= 63 elements and
+// there are kLocal / 64 of them: sub-segment j is finished by wave j with
+// shuffles, a packed wave scan and ds_permute (no block barriers, no LDS);
+// same rules, same tree.
+constexpr int kLocalWaveLevel = kLocalLog - 6;
+static_assert(kLocalLog >= 8 && kLocalLog <= 10, "sub-segment sizes are packed in 10-bit fields");
+static_assert(kLocal / 64 == (1 << kLocalWaveLevel), "one wave per wave-level sub-segment");
 
 // The selection build's elements: four SoA arrays (x, y, z, index bits) per
 // buffer k (0 / 1), unsorted inside each subtree range.
@@ -606,7 +618,7 @@ __device__ __forceinline__ uint64_t wave_minmax64(uint64_t v) {
 __device__ __forceinline__ void block_bitonic(uint64_t& k, int& v, int n2, uint64_t* kx, int16_t* vx) {
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int ls = 1; ls <= 10; ls++) {   // size 2 .. 1024, every stride a constant after unrolling
+  for (int ls = 1; ls <= kLocalLog; ls++) {   // size 2 .. kLocal, every stride a constant after unrolling
     const int size = 1 << ls;
 #pragma unroll
     for (int lst = ls - 1; lst >= 0; lst--) {
@@ -647,7 +659,7 @@ __device__ __forceinline__ void block_bitonic(uint64_t& k, int& v, int n2, uint6
 __device__ __forceinline__ void block_bitonic3(uint64_t (&k)[3], int (&v)[3], int n2, uint64_t* kx, int16_t* vx) {
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int ls = 1; ls <= 10; ls++) {
+  for (int ls = 1; ls <= kLocalLog; ls++) {
     const int size = 1 << ls;
 #pragma unroll
     for (int lst = ls - 1; lst >= 0; lst--) {
@@ -697,11 +709,12 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                                                                                            float4* __restrict__ nodes) {
   __shared__ float4 buf[3][kLocal];
   __shared__ int16_t tag[kLocal];
-  __shared__ int16_t sb[2][kLocal / 2], ss[2][kLocal / 2];   // sub-segment start / size, ping-pong by level
-  __shared__ int16_t sls[kLocal / 2];
-  __shared__ uint8_t sdim[kLocal / 2];
-  __shared__ float sco[kLocal / 2];
-  __shared__ int32_t sid[kLocal / 2];
+  constexpr int NS = 1 << kLocalWaveLevel;   // sub-segments at the wave level
+  __shared__ int16_t sb[2][NS], ss[2][NS];   // sub-segment start / size, ping-pong by level
+  __shared__ int16_t sls[NS / 2];
+  __shared__ uint8_t sdim[NS / 2];
+  __shared__ float sco[NS / 2];
+  __shared__ int32_t sid[NS / 2];
   __shared__ uint64_t sh[kLocal / 64 + 1];
   __shared__ uint64_t spre[1 << kLocalWaveLevel];   // packed-count prefix at each sub-segment's start
   __shared__ float4 stage[kLocal];   // this subtree's nodes by local heap index (w = -1: none)
@@ -1887,7 +1900,7 @@ __global__ __launch_bounds__(kSelThreads) PM_WAVES_ATTR(PM_KS_PART_WAVES) void k
 static hipError_t kd_build_sel(const float4* elems, int64_t n, float4* nodes, hipStream_t s) {
   int H = 0;
   while ((1ll << H) <= n) H++;          // levels = floor(log2 n) + 1
-  const int L0 = std::max(0, H - 10);   // subtrees at L0 hold <= 1023 elements
+  const int L0 = std::max(0, H - kLocalLog);   // subtrees at L0 hold <= kLocal - 1 elements
   const int64_t cap = 1ll << (L0 + 1);  // subtree records down to level L0
   int idbits = 1;
   while ((1ll << idbits) < n) idbits++;
@@ -2024,7 +2037,7 @@ static hipError_t kd_build_lists(const float4* elems, int64_t n, float4* nodes, 
   PM_HIP_TRY(hipMemcpyAsync(tsel.p, &root[2], 4, hipMemcpyHostToDevice, s));
   // segments at L0 hold <= 1023 elements; the check variant keeps every level
   // global (the identical-tree test compares the two libraries)
-  const int L0 = PM_CHECK_VARIANT ? H : std::max(0, H - 10);
+  const int L0 = PM_CHECK_VARIANT ? H : std::max(0, H - kLocalLog);
   for (int L = 0; L < H; L++) {
     if (L == L0) {
       k_kd_local<false><<<(int)(1ll << L0), kLocal, 0, s>>>(Lst, KdSoa{}, L0, T, nodes);
