@@ -548,6 +548,27 @@ __device__ __forceinline__ v3 radiance_g(const double (&list)[kKNearest], const 
 #define PM_GATHER_QL 8
 #endif
 constexpr int kSeedStride = PM_SEED_STRIDE;
+// Leader groups (k = 50 gather): walk ranks are dealt in blocks of G * S and the
+// first G ranks of each block lead, so a leader wave's lanes come in runs of G
+// neighbours that share cache lines (G = 1: every S-th rank; the wide gather
+// keeps G = 1). Followers consult the two leaders before and the two after them.
+// Measured (round 5, config 3's global gather): G = 1 / 4 / 8 / 16 41.4-41.5 /
+// 42.9-43.0 / 43.6-43.9 / 44.5 ms; at G = 8 the leader launch 5.95 -> 5.06 ms,
+// the followers 35.4 -> 38.6 ms (their seeds come from farther away): 1.
+#ifndef PM_SEED_GROUP
+#define PM_SEED_GROUP 1
+#endif
+constexpr int kSeedGroup = PM_SEED_GROUP;
+template <int G>
+struct Seeds {
+  static constexpr int64_t GS = (int64_t)G * kSeedStride;
+  static_assert(G >= 1 && kSeedStride >= 2, "a block holds G leaders and at least one follower each");
+  __host__ __device__ static int64_t count(int64_t nq) { return (nq / GS) * G + (nq % GS < G ? nq % GS : G); }
+  __device__ static int64_t leader_rank(int64_t l) { return (l / G) * GS + l % G; }
+  __device__ static int64_t follower_rank(int64_t t) { return (t / (GS - G)) * GS + G + t % (GS - G); }
+  __device__ static int64_t index(int64_t r) { return (r / GS) * G + r % GS; }   // r: a leader's rank
+  __device__ static int64_t before(int64_t r) { return (r / GS) * G + G - 1; }   // r: a follower's rank
+};
 constexpr int kSeedLeaders = PM_SEED_LEADERS;
 constexpr int kGatherQL = PM_GATHER_QL;   // LDS insert-queue depth
 // Leader step budget (wave iterations; 0: none). A leader wave ends when its
@@ -620,9 +641,10 @@ __device__ __forceinline__ float seed_cut(double bound, float r2) {
 }
 
 // cut-off of walk rank r (a follower) from the leaders' records
+template <int G>
 __device__ __forceinline__ float follower_cut(const float4* __restrict__ lead, int64_t nq, int64_t r, v3 q,
                                               float R2) {
-  const int64_t jp = r / kSeedStride, ns = (nq - 1) / kSeedStride + 1;
+  const int64_t jp = Seeds<G>::before(r), ns = Seeds<G>::count(nq);
   double b = seed_bound(lead[jp], q);
   if (jp + 1 < ns) b = fmin(b, seed_bound(lead[jp + 1], q));
   if (kSeedLeaders > 2) {
@@ -675,7 +697,7 @@ __device__ __forceinline__ float subtree_cut(const float4* __restrict__ nodes, u
 }
 
 // One level of the seeded gather. LEADERS: walk ranks 0, S, 2S, ... with the
-// plain cut-off, recording (position, K-th d^2) in lead[r / S]; followers:
+// plain cut-off, recording (position, K-th d^2) in lead[Seeds::index(r)]; followers:
 // every other rank (thread t -> rank (t / (S-1)) * S + 1 + t % (S-1)), cut-off
 // from the leaders. TAG only separates the global-map launches into their own
 // kernel symbol (rocprof). perm: lane of walk rank r takes query perm[r] and
@@ -702,7 +724,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
     r = valid ? (int64_t)retry[e] : 0;
   } else {
     const int64_t t = ((int64_t)bid - nrb) * blockDim.x + threadIdx.x;
-    r = LEADERS ? t * kSeedStride : (t / (kSeedStride - 1)) * kSeedStride + 1 + t % (kSeedStride - 1);
+    r = LEADERS ? Seeds<kSeedGroup>::leader_rank(t) : Seeds<kSeedGroup>::follower_rank(t);
     valid = t < t1 && r < nq;
   }
   if (redo_lane && ballot(valid) == 0) return;   // wave-uniform: no retry entry for this wave
@@ -717,11 +739,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
       // that list's last d^2: its 50 points lie within it, so it bounds the
       // 50th nearest (and admits it: only d^2 <= cut are candidates)
       if (redo_lane && kLeaderSoft) {
-        const float t = lead[r / kSeedStride].w;
+        const float t = lead[Seeds<kSeedGroup>::index(r)].w;
         if (t >= 0.f) cut = fminf(cut, t);
       }
     } else {
-      cut = follower_cut(lead, nq, r, q, R2);
+      cut = follower_cut<kSeedGroup>(lead, nq, r, q, R2);
     }
   }
   double list[kKNearest];
@@ -741,14 +763,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
     const bool full = gkey_word(list[kKNearest - 1]) != kNoWord;
     const v3 f = radiance_g(list, payload, qq.w, full ? gkey_d2(list[kKNearest - 1]) : R2);
     out[i] = make_float4(f.x, f.y, f.z, 0.f);
-    if (LEADERS) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, full ? gkey_d2(list[kKNearest - 1]) : -1.f);
+    if (LEADERS) lead[Seeds<kSeedGroup>::index(r)] = make_float4(qq.x, qq.y, qq.z, full ? gkey_d2(list[kKNearest - 1]) : -1.f);
   }
   if (LEADERS && kLeaderBudget > 0) {
     const bool redo = valid && aborted;
     // a cut-off walk's full list still bounds the 50th nearest (any 50 points
     // do): its last d^2 seeds the followers and the retry; not full: nothing
     const bool part_full = kLeaderSoft && gkey_word(list[kKNearest - 1]) != kNoWord;
-    if (redo) lead[r / kSeedStride] = make_float4(qq.x, qq.y, qq.z, part_full ? gkey_d2(list[kKNearest - 1]) : -1.f);
+    if (redo) lead[Seeds<kSeedGroup>::index(r)] = make_float4(qq.x, qq.y, qq.z, part_full ? gkey_d2(list[kKNearest - 1]) : -1.f);
     const uint64_t m = ballot(redo);
     if (m != 0) {   // wave-aggregated append to the retry list
       const int lane = threadIdx.x & 63, first = __ffsll((long long)m) - 1;
@@ -838,7 +860,7 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   else k_gather_plain<0><<<g, 256, 0, s>>>(m->nodes.p, m->payload.p, n, qb, nq, out, perm);
   return hipGetLastError();
 #else
-  const int64_t nl = (nq + kSeedStride - 1) / kSeedStride;   // leaders: walk ranks 0, S, 2S, ...
+  const int64_t nl = Seeds<kSeedGroup>::count(nq);   // leaders: walk ranks 0, S, 2S, ... (G = 1)
   DevBuf<float4> lead(nl);
   DevBuf<uint32_t> retry(kLeaderBudget > 0 ? nl : 0), nretry(kLeaderBudget > 0 ? 1 : 0);
   if (!lead.p || (kLeaderBudget > 0 && (!retry.p || !nretry.p))) return hipErrorOutOfMemory;
@@ -1189,7 +1211,7 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
         const float ts = lead[r / kSeedStride].w;
         if (ts >= 0.f) cut = fminf(cut, ts);
       } else {
-        cut = follower_cut(lead, nq, r, q, R2);
+        cut = follower_cut<1>(lead, nq, r, q, R2);
       }
     }
     double tail = gkey(cut, kNoWord);
