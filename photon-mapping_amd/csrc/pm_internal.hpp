@@ -45,7 +45,9 @@ struct pm_photon_map {
 // alternate path that must give bit-identical results in one library -- the
 // plain kNN walk instead of the leader-seeded one, all-global kd levels instead
 // of the LDS finish, the Karras LBVH instead of PLOC, a one-slot first guess
-// for the render's continuation vertices (always rerun) -- plus a 4-entry LDS
+// for the render's continuation vertices (always rerun), the per-bounce
+// wavefront photon trace instead of the fused paths (the Makefile's check
+// target sets PM_TRACE_FUSED=0) -- plus a 4-entry LDS
 // traversal stack (PM_STACK_DEPTH=4: nearly every ray spills to scratch).
 // tests/test_gpu_check_variant.py compares it with the production library.
 #ifndef PM_CHECK_VARIANT

@@ -36,23 +36,91 @@ struct PhotonRay {   // 48 B
   float4 c;          // colour, (deposits << 8 | bounce) (bits)
 };
 
+// Emission of photon i of this call (global index g_lo + i): pointLightRayGen
+// (photon-mapping/cuda/deviceCode.cu:54-72), RNG seeded with the per-light id.
+__device__ __forceinline__ void ph_emit(const LightDev* __restrict__ lights, const int64_t* __restrict__ loff, int nl,
+                                        int64_t g, uint32_t& rng, v3& o, v3& d, v3& color) {
+  int l = 0;
+  while (l < nl - 1 && g >= loff[l + 1]) l++;
+  const uint32_t id = (uint32_t)(g - loff[l]);
+  const LightDev L = lights[l];
+  rng = lcg_init(id, 0u);
+  emit_photon(L.rgb.w, v3{L.pos.x, L.pos.y, L.pos.z}, v3{L.nrm.x, L.nrm.y, L.nrm.z}, L.nrm.w, rng, o, d);
+  color = v3{L.rgb.x, L.rgb.y, L.rgb.z};
+}
+
+// One photon event at the end of a segment (t, slot: the closest hit; slot < 0:
+// miss): triangleMeshClosestHit (deviceCode.cu:113-131) picks the event, and
+// shootPhoton / shootCausticsPhoton (:25-52) deposit and decide whether the path
+// goes on. Deposit k of photon pi lands in slots[k][pi]; a path that ends writes
+// its deposit count to cnt[pi]. Returns true with the continuation (so, sd, and
+// the scattered colour in `color`) when the path goes on to bounce b + 1.
+__device__ __forceinline__ bool ph_event(const DevScene& S, v3 o, v3 d, float t, int slot, uint32_t& rng, v3& color,
+                                         uint32_t& n, int b, uint32_t pi, int64_t np, int maxd, int caustic,
+                                         pm_photon* __restrict__ slots, uint32_t* __restrict__ cnt, v3& so, v3& sd) {
+  int ev;
+  v3 sc = {0.f, 0.f, 0.f};
+  so = sd = v3{0.f, 0.f, 0.f};
+  if (slot < 0) {
+    ev = EV_MISS;
+  } else {
+    const int mesh = __float_as_int(S.tri[3 * slot].w);
+    const float4 m0 = S.mat[2 * mesh], m1 = S.mat[2 * mesh + 1];
+    const float pd = m0.w;
+    const float ps = m1.x + pd;
+    const float pt = m1.y + ps;
+    const float rp = lcg_next(rng);
+    const v3 hp = add(o, smul(t, d));
+    const v3 albedo = {m0.x, m0.y, m0.z};
+    if (rp < pd) {
+      ev = EV_DIFFUSE;
+      so = hp;
+      sd = cosine_sample_hemisphere(tri_normal(S, slot), rng);
+      sc = mulv(albedo, color);
+    } else if (rp < ps) {
+      ev = EV_SPECULAR;
+      so = hp;
+      sd = reflect(d, tri_normal(S, slot));
+      sc = mulv(albedo, color);
+    } else if (rp < pt) {
+      ev = EV_REFRACT;
+      so = hp;
+      sd = refract_ior(d, tri_normal(S, slot), m1.z);
+      sc = mulv(albedo, color);
+    } else {
+      ev = EV_ABSORBED;
+    }
+  }
+  if (b > 0 && ev == EV_DIFFUSE) {
+    pm_photon p;
+    p.pos = {so.x, so.y, so.z};
+    p.dir = {sd.x, sd.y, sd.z};
+    p.power = 0;
+    p.color = {color.x, color.y, color.z};
+    slots[(int64_t)n * np + pi] = p;
+    n++;
+  }
+  const bool cont = caustic ? ((ev & (EV_SPECULAR | EV_REFRACT)) != 0) : (ev == EV_DIFFUSE);
+  if (!cont || b + 1 >= maxd) {
+    cnt[pi] = n;
+    return false;
+  }
+  color = sc;
+  return true;
+}
+
 __global__ __launch_bounds__(256) void k_ph_gen(const LightDev* __restrict__ lights, const int64_t* __restrict__ loff,
                                                 int nl, int64_t g_lo, int64_t np, PhotonRay* __restrict__ rays) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= np) return;
   // pointLightRayGen (photon-mapping/cuda/deviceCode.cu:54-72)
-  const int64_t g = g_lo + i;
-  int l = 0;
-  while (l < nl - 1 && g >= loff[l + 1]) l++;
-  const uint32_t id = (uint32_t)(g - loff[l]);
-  const LightDev L = lights[l];
-  uint32_t rng = lcg_init(id, 0u);
-  v3 o, d;
-  emit_photon(L.rgb.w, v3{L.pos.x, L.pos.y, L.pos.z}, v3{L.nrm.x, L.nrm.y, L.nrm.z}, L.nrm.w, rng, o, d);
+  uint32_t rng;
+  v3 o, d, c;
+  ph_emit(lights, loff, nl, g_lo + i, rng, o, d, c);
   PhotonRay r;
   r.o = make_float4(o.x, o.y, o.z, __uint_as_float(rng));
   r.d = make_float4(d.x, d.y, d.z, __uint_as_float((uint32_t)i));
-  r.c = make_float4(L.rgb.x, L.rgb.y, L.rgb.z, __uint_as_float(0u));
+  r.c = make_float4(c.x, c.y, c.z, __uint_as_float(0u));
   rays[i] = r;
 }
 
@@ -111,58 +179,13 @@ __global__ __launch_bounds__(kShadeBlock) void k_ph_shade(DevScene S, const Phot
     const uint32_t nb = __float_as_uint(pr.c.w);
     uint32_t n = nb >> 8;
     const int b = (int)(nb & 0xFF);
-    const v3 o = {pr.o.x, pr.o.y, pr.o.z}, d = {pr.d.x, pr.d.y, pr.d.z}, color = {pr.c.x, pr.c.y, pr.c.z};
-    int ev;
-    v3 so = {0.f, 0.f, 0.f}, sd = {0.f, 0.f, 0.f}, sc = {0.f, 0.f, 0.f};
-    // triangleMeshClosestHit (deviceCode.cu:113-131)
-    if (slot < 0) {
-      ev = EV_MISS;
-    } else {
-      const int mesh = __float_as_int(S.tri[3 * slot].w);
-      const float4 m0 = S.mat[2 * mesh], m1 = S.mat[2 * mesh + 1];
-      const float pd = m0.w;
-      const float ps = m1.x + pd;
-      const float pt = m1.y + ps;
-      const float rp = lcg_next(rng);
-      const v3 hp = add(o, smul(hh.x, d));
-      const v3 albedo = {m0.x, m0.y, m0.z};
-      if (rp < pd) {
-        ev = EV_DIFFUSE;
-        so = hp;
-        sd = cosine_sample_hemisphere(tri_normal(S, slot), rng);
-        sc = mulv(albedo, color);
-      } else if (rp < ps) {
-        ev = EV_SPECULAR;
-        so = hp;
-        sd = reflect(d, tri_normal(S, slot));
-        sc = mulv(albedo, color);
-      } else if (rp < pt) {
-        ev = EV_REFRACT;
-        so = hp;
-        sd = refract_ior(d, tri_normal(S, slot), m1.z);
-        sc = mulv(albedo, color);
-      } else {
-        ev = EV_ABSORBED;
-      }
-    }
-    // shootPhoton / shootCausticsPhoton (deviceCode.cu:25-52)
-    if (b > 0 && ev == EV_DIFFUSE) {
-      pm_photon p;
-      p.pos = {so.x, so.y, so.z};
-      p.dir = {sd.x, sd.y, sd.z};
-      p.power = 0;
-      p.color = {color.x, color.y, color.z};
-      slots[(int64_t)n * np + pi] = p;
-      n++;
-    }
-    const bool cont = caustic ? ((ev & (EV_SPECULAR | EV_REFRACT)) != 0) : (ev == EV_DIFFUSE);
-    if (!cont || b + 1 >= maxd) {
-      cnt[pi] = n;
-    } else {
+    v3 color = {pr.c.x, pr.c.y, pr.c.z}, so, sd;
+    if (ph_event(S, v3{pr.o.x, pr.o.y, pr.o.z}, v3{pr.d.x, pr.d.y, pr.d.z}, hh.x, slot, rng, color, n, b, pi, np,
+                 maxd, caustic, slots, cnt, so, sd)) {
       keep = true;
       nr.o = make_float4(so.x, so.y, so.z, __uint_as_float(rng));
       nr.d = make_float4(sd.x, sd.y, sd.z, __uint_as_float(pi));
-      nr.c = make_float4(sc.x, sc.y, sc.z, __uint_as_float((n << 8) | (uint32_t)(b + 1)));
+      nr.c = make_float4(color.x, color.y, color.z, __uint_as_float((n << 8) | (uint32_t)(b + 1)));
     }
   }
   // block-aggregated append
@@ -182,6 +205,123 @@ __global__ __launch_bounds__(kShadeBlock) void k_ph_shade(DevScene S, const Phot
   for (int w = 0; w < wave; w++) off += wcount[w];
   const uint32_t dst = off + (uint32_t)__popcll(m & ((1ull << lane) - 1));
   out[dst] = nr;
+}
+
+// ------------------------------------------------------------------ fused paths
+// PM_TRACE_FUSED: one launch per chunk instead of emission + two per bounce.
+// A persistent grid (PM_TPATH_BLOCKS workgroups per CU) takes photons from a
+// global counter; each lane traces a photon's whole path: emission, then per
+// segment the same closest-hit traversal as k_ph_trace_pool and the same event
+// as k_ph_shade (ph_event), continuing with the scattered ray until the path
+// ends, then takes the next photon. Lanes whose segment is done wait until
+// PM_PATH_EVENT_MIN of them (or all the wave's non-idle lanes) are, and the
+// wave runs their events together; idle lanes are refilled together (one
+// atomic per wave). Deposits land in slots[k][photon] as before, so the output
+// is the wavefront path's bit for bit (the check variant library keeps the
+// wavefront path: tests/test_gpu_check_variant.py compares the two). A grid of
+// one workgroup per 128 photons held every wave slot for the whole trace; the
+// cap below can leave slots and VGPRs to kernels on other streams.
+// Config 3's global trace alone: ~19 ms (the wavefront path: ~27 ms).
+#ifndef PM_TRACE_FUSED
+#define PM_TRACE_FUSED 1
+#endif
+#ifndef PM_PATH_EVENT_MIN
+#define PM_PATH_EVENT_MIN 16
+#endif
+#ifndef PM_TPATH_WAVES
+#define PM_TPATH_WAVES 7
+#endif
+// Workgroups of kTBlock threads per CU (14: every slot 72 VGPRs allow, 7 waves
+// per SIMD). Config 3 frames (ms) with the render begin beside the trace, caps
+// 6 / 8 / 10 / 14: 97.7 / 97.0 / 97.0 / 98.4 (wavefront trace: 96.5); with the
+// render begin after the trace (FrameConfig.begin_after_trace, now the
+// default): 8 / 10 / 14: 99.1 / 97.9 / 93.8-94.3.
+#ifndef PM_TPATH_BLOCKS
+#define PM_TPATH_BLOCKS 14
+#endif
+__global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TPATH_WAVES) void k_ph_paths(
+    DevScene S, const LightDev* __restrict__ lights, const int64_t* __restrict__ loff, int nl, int64_t g_lo,
+    int64_t np, int maxd, int caustic, pm_photon* __restrict__ slots, uint32_t* __restrict__ cnt,
+    unsigned long long* __restrict__ next, int* overflow) {
+  __shared__ int stack[kStackDepth * kTBlock];
+  int* const st = stack + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int spill[kSpillDepth > 0 ? kSpillDepth : 1];
+  Ray r;
+  HitInfo h{kPhotonTmax, -1, -1};
+  int node = 0, sp = 0, b = 0;
+  int64_t pi = -1;      // this lane's photon (-1: idle)
+  bool pend = false;    // its segment's traversal is done, the event not yet run
+  uint32_t rng = 0, n = 0;
+  v3 color = {0.f, 0.f, 0.f};
+  bool drained = false;
+  for (;;) {
+    const uint64_t pm = __ballot(pend);
+    if (pm != 0 && (__popcll(pm) >= PM_PATH_EVENT_MIN || __ballot(pi >= 0 && !pend) == 0)) {
+      if (pend) {
+        v3 so, sd;
+        if (ph_event(S, r.o, r.d, h.t, h.slot, rng, color, n, b, (uint32_t)pi, np, maxd, caustic, slots, cnt, so,
+                     sd)) {
+          ray_prep(r, so, sd);
+          h = HitInfo{kPhotonTmax, -1, -1};
+          node = 0;
+          sp = 0;
+          b++;
+        } else {
+          pi = -1;
+        }
+        pend = false;
+      }
+    }
+    const uint64_t idle = __ballot(pi < 0);
+    const int nidle = __popcll(idle);
+    if (!drained && nidle >= PM_POOL_REFILL) {
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(next, (unsigned long long)nidle);
+      base = __shfl(base, 0);
+      if (base + (unsigned long long)nidle >= (unsigned long long)np) drained = true;
+      if (pi < 0) {
+        const int64_t i = (int64_t)base + __popcll(idle & lt_mask);
+        if (i < np) {
+          v3 o, d;
+          ph_emit(lights, loff, nl, g_lo + i, rng, o, d, color);
+          ray_prep(r, o, d);
+          h = HitInfo{kPhotonTmax, -1, -1};
+          node = 0;
+          sp = 0;
+          b = 0;
+          n = 0;
+          pi = i;
+          pend = S.ntri <= 0;   // empty scene: a miss at once
+        }
+      }
+    }
+    if (__ballot(pi >= 0) == 0) {
+      if (drained) break;
+      continue;
+    }
+    if (pi >= 0 && !pend && traverse_step<false>(S, r, kEPS, kPhotonTmax, st, kTBlock, spill, node, sp, h, overflow))
+      pend = true;
+  }
+}
+
+static hipError_t launch_trace_fused(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl,
+                                     int64_t g_lo, int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt,
+                                     hipStream_t s) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  DevBuf<unsigned long long> next(1);
+  if (!next.p) return hipErrorOutOfMemory;
+  PM_HIP_TRY(hipMemsetAsync(next.p, 0, sizeof(unsigned long long), s));
+  const int64_t want = (np + kTBlock - 1) / kTBlock;
+  const int grid = (int)std::min<int64_t>(want, (int64_t)cus * PM_TPATH_BLOCKS);
+  k_ph_paths<<<grid, kTBlock, 0, s>>>(sc->view(), d_lights, d_loff, nl, g_lo, np, maxd, caustic, slots, cnt, next.p,
+                                      sc->overflow.p);
+  PM_HIP_TRY(hipGetLastError());
+  return hipStreamSynchronize(s);   // the counter is freed on return
 }
 
 __global__ void k_live_init(uint32_t* __restrict__ live, int nlive, uint32_t np) {
@@ -250,6 +390,7 @@ hipError_t launch_trace_chunk(pm_scene* sc, const LightDev* d_lights, const int6
   if (np <= 0) return hipSuccess;
   if (maxd <= 0) return hipMemsetAsync(cnt, 0, sizeof(uint32_t) * np, s);
   if (np > 0xFFFFFFFFll) return hipErrorInvalidValue;   // photon ids and live counts are 32-bit
+  if (PM_TRACE_FUSED) return launch_trace_fused(sc, d_lights, d_loff, nl, g_lo, np, maxd, caustic, slots, cnt, s);
   return launch_trace_wavefront(sc, d_lights, d_loff, nl, g_lo, np, maxd, caustic, slots, cnt, s);
 }
 

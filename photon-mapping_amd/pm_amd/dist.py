@@ -59,11 +59,20 @@ class FrameConfig:
     # the caustic map (pm_render_gather_caustic), i.e. beside the global map's
     # kd build, instead of beside the global gather in finish
     early_caustic_gather: bool = False
-    # one rank: the render side thread traces the caustic photons and builds
-    # their map beside the global trace, then holds pm_render_begin until the
-    # global trace is done, so the render's latency-bound ray kernels run beside
-    # the bandwidth-bound kd build instead of beside the trace
-    begin_after_trace: bool = False
+    # the render side thread traces the caustic photons (one rank: and builds
+    # their map) beside the global trace, then holds pm_render_begin until the
+    # global trace is done, so the render's ray kernels run beside the exchange
+    # and the kd build instead of beside the trace. Default since the fused
+    # photon-path kernel (csrc/trace.hip, PM_TRACE_FUSED), which holds every wave
+    # slot it can get for the whole trace: the render begin beside it stretched
+    # to 33 ms (config 3: 93.8-94.3 vs 98.4-99.0 ms per frame; the wavefront
+    # trace with the render begin beside it: 96.3-96.6 ms)
+    begin_after_trace: bool = True
+    # one rank: the caustic photons are traced, and their map built, on the main
+    # thread right after the global trace (the side thread runs pm_render_begin
+    # only): for a global trace short enough that the caustic work would
+    # otherwise wait behind the render begin
+    caustic_after_trace: bool = False
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -461,7 +470,7 @@ class GpuBackend:
                     box["r"] = (j, pm.phase_us("paths"))   # phase timers are per host thread
                     return j
 
-                late = c.begin_after_trace and caustic_shard is not None and caustic_map
+                late = c.begin_after_trace and caustic_shard is not None
                 if not late:
                     job = begin()
                 if caustic_shard is not None:
@@ -473,11 +482,11 @@ class GpuBackend:
                     if caustic_map:
                         cm = pm.PhotonMap(t, pm.CAUSTICS_PHOTON_POWER, stream=side.cuda_stream)
                         box["cm"] = (cm, pm.phase_us("kdbuild"))
-                        if late:
-                            box["trace_done"].wait()
-                            job = begin()
-                        if c.early_caustic_gather:
-                            job.gather_caustic(cm, stream=side.cuda_stream)
+                    if late:
+                        box["trace_done"].wait()
+                        job = begin()
+                    if caustic_map and c.early_caustic_gather:
+                        job.gather_caustic(cm, stream=side.cuda_stream)
             except BaseException as e:   # re-raised by finish_render / join_render
                 box["e"] = e
             finally:
@@ -553,10 +562,13 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     backend.phase = {}
     pending = None
     if backend.cfg.overlap_render and hasattr(backend, "start_render"):
-        early_caustic = world == 1 and not backend.cfg.quantize
-        pending = backend.start_render(rank, world, caustic_shard=(rank, world), caustic_map=early_caustic)
+        side_caustic = not (world == 1 and backend.cfg.caustic_after_trace)
+        early_caustic = world == 1 and not backend.cfg.quantize and side_caustic
+        pending = backend.start_render(rank, world, caustic_shard=(rank, world) if side_caustic else None,
+                                       caustic_map=early_caustic)
     try:
-        g, c, gm, cm = _maps(backend, rank, world, dist, pending, pending is not None and early_caustic)
+        g, c, gm, cm = _maps(backend, rank, world, dist, pending, pending is not None and early_caustic,
+                             side_caustic=pending is not None and side_caustic)
     except BaseException:
         if pending is not None:   # no side work outlives a failed frame
             try:
@@ -594,15 +606,17 @@ def nrows(x) -> int:
     return int(x.n if hasattr(x, "segments") else x.shape[0])
 
 
-def _maps(backend, rank: int, world: int, dist, pending=None, early_caustic: bool = False):
+def _maps(backend, rank: int, world: int, dist, pending=None, early_caustic: bool = False, side_caustic=None):
     """Trace both photon sets, exchange them (N > 1), build both maps. With a
-    render pending from start_render(caustic_shard=...), the caustic photons
-    come from its thread; with early_caustic (world 1), so does the caustic map
-    (returned as None here)."""
+    render pending from start_render(caustic_shard=...) (side_caustic), the
+    caustic photons come from its thread; with early_caustic (world 1), so does
+    the caustic map (returned as None here)."""
+    if side_caustic is None:
+        side_caustic = pending is not None
     g = backend.trace(False, rank, world)
     if pending is not None and hasattr(backend, "trace_done"):
         backend.trace_done(pending)
-    c = backend.caustic_photons(pending) if pending is not None else backend.trace(True, rank, world)
+    c = backend.caustic_photons(pending) if side_caustic else backend.trace(True, rank, world)
     if backend.cfg.quantize:   # elementwise: the same before or after the exchange
         g, c = backend.quantize(g), backend.quantize(c)
     sel = None

@@ -9,7 +9,8 @@ measure: the RCCL all-gathers over xGMI at an assumed receive bandwidth.
 
   WORLDS="2 4 8"  CONFIG=3|5  XGMI_GBS="300 450"  (effective all-gather receive
   bandwidth per GPU, GB/s; MI355X: 7 xGMI links per GPU)  RANKS="0 2" (ranks to
-  run; default all)  REPS=2 (frames per rank, the last is reported)"""
+  run; default all)  REPS=2 (frames per rank, the last is reported)
+  FRAME_OPTS="begin_after_trace=0" (boolean FrameConfig fields, comma-separated)"""
 import json
 import os
 import sys
@@ -36,6 +37,9 @@ bws = [float(x) for x in os.environ.get("XGMI_GBS", "300 450").split()]
 for world in [int(x) for x in os.environ.get("WORLDS", "2 4 8").split()]:
     cfg = pmdist.FrameConfig(casted=per_gpu[0] * world, caustic=per_gpu[1] * world, width=1920, height=1080,
                              camera=CAMERA, caustic_k=caustic_k)
+    for opt in filter(None, os.environ.get("FRAME_OPTS", "").split(",")):
+        k, v = opt.split("=")
+        setattr(cfg, k, v == "1")
     t0 = time.time()
     rec = replay.record(scene, lights, cfg, world, keep_map=False)
     t_rec = time.time() - t0
