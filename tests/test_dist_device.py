@@ -40,8 +40,9 @@ class _StubPM:
         return "cmap"
 
 
+@pytest.mark.parametrize("after", [True, False])
 @pytest.mark.parametrize("device", ["cuda:3", "cuda:7"])
-def test_start_render_thread_sets_rank_device_first(monkeypatch, device):
+def test_start_render_thread_sets_rank_device_first(monkeypatch, device, after):
     import torch
     from pm_amd import dist
 
@@ -52,12 +53,18 @@ def test_start_render_thread_sets_rank_device_first(monkeypatch, device):
     be = dist.GpuBackend.__new__(dist.GpuBackend)
     be.pm = _StubPM(log)
     be.scene, be.lights, be.cam, be.cbuf = object(), [], object(), None
-    be.cfg = dist.FrameConfig(casted=10, caustic=10)
+    be.cfg = dist.FrameConfig(casted=10, caustic=10, begin_after_trace=after)
     be.phase = {}
     pending = be.start_render(3, 8, caustic_shard=(3, 8), caustic_map=True)
+    be.trace_done(pending)   # what _maps does once the global trace is over
     job, _ = be.join_render(pending)
     assert job is not None
     assert log[0][0] == "set_device" and log[0][1] == device, log
     assert log[0][2] == "pm-render-begin"      # in the side thread, not the caller's
-    assert [e[0] for e in log] == ["set_device", "render_begin", "trace", "map"], log
-    assert log[2][1] == 0x1234 and log[3][1] == 0x1234   # the trace and map run on the side stream
+    # begin_after_trace (default): the caustic trace and map first, the render
+    # begin once the global trace is done
+    order = ["trace", "map", "render_begin"] if after else ["render_begin", "trace", "map"]
+    assert [e[0] for e in log] == ["set_device"] + order, log
+    for e in log[1:]:
+        if e[0] != "render_begin":
+            assert e[1] == 0x1234   # the trace and map run on the side stream
