@@ -12,7 +12,10 @@ switches every gather walk to subtree-box skips after one iteration
 reach), so the box path runs on all of them, addresses kd nodes with 64
 bits (PM_FORCE_WIDE=1; production: maps of >= 2^28 nodes only), and builds
 every kd-tree with the selection build (PM_KD_SEL_MIN=0; production: maps of
->= 2^24 elements, the presorted build below), so its trees of these small
+>= 2^24 elements, the presorted build below), and keeps only 4 traversal-stack
+entries in LDS (PM_STACK_DEPTH=4: the fused photon-path kernel and the render's
+ray pools spill to scratch on the deep-stack scene; the check variant, which
+also has a 4-entry stack, traces photons with the per-bounce wavefront path), so its trees of these small
 workloads (ties, duplicates, one repeated point, axis planes, signed zeros
 and infinities) must equal production's presorted ones. The lists
 and radiance must not depend on any of it: the small workloads of tests/variant_workloads.py (seeded
@@ -34,7 +37,7 @@ PKG = os.path.join(conftest.ROOT, "photon-mapping_amd")
 VARIANT = os.path.join(PKG, "lib_budget", "libpm_hip.so")
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-KEYS = ["gather_g", "gather_c", "gather_e", "gather_k200", "gather_k256", "render_64_rgba", "render_64_rgb", "render_64_stats", "render_40_rgba",
+KEYS = ["cloud_hits", "cloud_occ", "cloud_photons", "cornell_g", "cornell_c", "gather_g", "gather_c", "gather_e", "gather_k200", "gather_k256", "render_64_rgba", "render_64_rgb", "render_64_stats", "render_40_rgba",
         "render_40_rgb", "render_40_stats", "sphere_rgb", "sphere_stats", "cornell_gmap", "cornell_cmap",
         "kd_5", "kd_1023", "kd_1024", "kd_70000", "kd_2000003", "kd_same_5000", "kd_wall_300001",
         "kd_special_70001"]
