@@ -309,9 +309,8 @@ __global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TPATH_WAVES) void k_ph_pa
 static hipError_t launch_trace_fused(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl,
                                      int64_t g_lo, int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt,
                                      hipStream_t s) {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+  int cus = 0;   // of the stream's device (a process may drive several)
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, stream_device(s)) != hipSuccess || cus <= 0)
     cus = 256;
   DevBuf<unsigned long long> next(1);
   if (!next.p) return hipErrorOutOfMemory;
