@@ -1981,10 +1981,15 @@ static hipError_t kd_build_sel(const float4* elems, int64_t n, float4* nodes, hi
 #define PM_KD_SEL 1   // the selection build (production); 0: the presorted build only
 #endif
 // Below this size the presorted build is faster (the selection build's ~10
-// launches per level dominate): 45.4 M elements 21.4 vs 24.5 ms, 10 M 6.0 vs
-// 5.7 ms, 1 M 2.0 vs 1.0 ms (tools/kd_probe.py). Same tree either way.
+// launches per level dominate). Round 3 (tools/kd_probe.py): 45.4 M elements
+// 21.4 vs 24.5 ms, 10 M 6.0 vs 5.7 ms, 1 M 2.0 vs 1.0 ms: 2^24. Round 5, the
+// current kernels (tools/kd_size_probe.py, uniform random points, selection vs
+// presorted): 2.2 M 1.99 vs 1.55 ms, 3 M 2.10 vs 1.85, 4 M 2.25 vs 2.25, 6 M
+// 3.17 vs 3.46, 8 M 3.60 vs 4.21, 12 M 5.84 vs 6.33, 16.8 M 6.81 vs 8.60: 2^22
+// (the 8-rank subtrees of 2^24 - 1 elements now take the selection build).
+// Same tree either way.
 #ifndef PM_KD_SEL_MIN
-#define PM_KD_SEL_MIN (1 << 24)
+#define PM_KD_SEL_MIN (1 << 22)
 #endif
 
 static hipError_t kd_build_lists(const float4* elems, int64_t n, float4* nodes, hipStream_t s);
