@@ -107,6 +107,20 @@ def test_trace_square_light_bitwise(cornell, caustics):
     assert len(pg) > 0 and np.array_equal(_bits(pg), _bits(po))
 
 
+@pytest.mark.parametrize("max_depth", [2, 3, 30])
+@pytest.mark.parametrize("caustics", [False, True])
+def test_trace_depth_bitwise(cornell, caustics, max_depth):
+    """Path-length limits: the fused path kernel (csrc/trace.hip k_ph_paths)
+    ends a path at bounce max_depth - 1 exactly as shootPhoton's loop does."""
+    import oracle
+    import pm_amd
+    meshes, lights = cornell
+    gs, os_ = _scene_pair(meshes)
+    pg = pm_amd.run_point_light_ray_gen(gs, lights, 20000, max_depth, caustics).cpu().numpy()
+    po = oracle.trace(os_, lights, 20000, max_depth, caustics)
+    assert pg.shape == po.shape and np.array_equal(_bits(pg), _bits(po))
+
+
 def test_trace_shards_concatenate(cornell):
     import pm_amd
     meshes, lights = cornell
