@@ -218,10 +218,13 @@ __global__ __launch_bounds__(kShadeBlock) void k_ph_shade(DevScene S, const Phot
 // wave runs their events together; idle lanes are refilled together (one
 // atomic per wave). Deposits land in slots[k][photon] as before, so the output
 // is the wavefront path's bit for bit (the check variant library keeps the
-// wavefront path: tests/test_gpu_check_variant.py compares the two). A grid of
-// one workgroup per 128 photons held every wave slot for the whole trace; the
-// cap below can leave slots and VGPRs to kernels on other streams.
-// Config 3's global trace alone: ~19 ms (the wavefront path: ~27 ms).
+// wavefront path: tests/test_gpu_check_variant.py compares the two; the budget
+// variant runs this kernel with a 4-entry LDS stack against production). The
+// kernel holds every wave slot it gets until the last path ends, so the frame
+// starts the render's ray kernels after it (pm_amd.dist FrameConfig.
+// begin_after_trace); the cap below can leave slots and VGPRs to other streams
+// instead (measured slower). Config 3's global trace alone:
+// ~16-17 ms (the wavefront path: ~27 ms).
 #ifndef PM_TRACE_FUSED
 #define PM_TRACE_FUSED 1
 #endif
