@@ -16,7 +16,6 @@
 // (list_insert), and the walk tests a node's point post-order so root-path
 // points meet a tight bound (knn_walk, knn_walk_lean; variants measured: DESIGN.md §4.4).
 #include <algorithm>
-#include <cfloat>
 #include <cmath>
 
 #include "pm_internal.hpp"
@@ -380,125 +379,6 @@ __device__ __forceinline__ void lean_step(const float4* __restrict__ nodes, uint
   nd = ndn;
 }
 
-// ---- Split keys (PM_GATHER_SKEY): the walk's descent on 4 B per node.
-// skey[c] = the f32 bits of node c's split coordinate with its two lowest
-// mantissa bits replaced by the split dimension (45.4 M nodes: 182 MB against
-// the 727 MB node array, so it stays in the 256-MB MALL and a 128-B line holds
-// 32 nodes instead of 8). The step decides its transitions from the split key
-// alone; a node's 16-B record (position + node word) is loaded only for a point
-// test whose plane gap is within the lane's bound, and tested one step later,
-// off the descent's dependent-load chain.
-// Exact: the stored float s~ and the split coordinate s differ only in those
-// two bits, so s lies between sa = s~ & ~3 and sb = s~ | 3 (either order by
-// sign). With da = q[dim] - sa and db = q[dim] - sb, every point p of the far
-// half-space has |q[dim] - p[dim]| >= g = max(right ? min(da, db) :
-// -max(da, db), 0) in f32 (rounding is monotone), and its d^2 >= g^2 (the
-// uncontracted sum of non-negative terms); the node's own point (on its plane)
-// too. So a far subtree or a point test skipped for g^2 > bound holds no key
-// below the lane's tail. Any side choice is exact (it only orders the visits).
-// Non-finite split coordinates are stored as +-FLT_MAX (NaN orders as +inf in
-// the build): the subtree beyond a +inf / NaN (-inf) plane holds only points
-// whose coordinate there is +inf / NaN (-inf), i.e. no finite d^2, while the
-// other side is every finite query's close side, never pruned.
-#ifndef PM_GATHER_SKEY
-#define PM_GATHER_SKEY 0   // measured slower (profiles/r06/r06a_skey_ab.log): 51.7 vs 41.4 ms
-#endif
-__global__ void k_split_keys(const float4* __restrict__ nodes, int64_t n, uint32_t* __restrict__ skey) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const float4 p = nodes[t];
-  const uint32_t dim = __float_as_uint(p.w) & 3u;
-  float s = dim == 0 ? p.x : (dim == 1 ? p.y : p.z);
-  if (!(fabsf(s) <= FLT_MAX)) s = s < 0.f ? -FLT_MAX : FLT_MAX;
-  skey[t] = (__float_as_uint(s) & ~3u) | dim;
-}
-// f32 a - b as one v_sub_f32 (never packed into a v_pk_add_f32)
-__device__ __forceinline__ float fsub_v(float a, float b) {
-  float r;
-  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-// split key of node c1 (1-based): 32-bit byte offsets below 2^28 nodes
-template <bool WIDE>
-__device__ __forceinline__ uint32_t skey1(const uint32_t* __restrict__ sk, uint32_t c1) {
-  if (WIDE) return sk[(size_t)c1 - 1];
-  return *(const uint32_t*)((const char*)sk - 4 + (c1 << 2));
-}
-// side (true: q beyond the plane, the right child is the close one) and the
-// plane gap lower bound g >= 0 of the far half-space and of the node's point
-struct SkPlane {
-  bool right;
-  float gap;
-};
-__device__ __forceinline__ SkPlane sk_plane(uint32_t sk, v3 q) {
-  const uint32_t dim = sk & 3u;
-  const float sa = __uint_as_float(sk & ~3u), sb = __uint_as_float(sk | 3u);
-  const float qd = dim == 0 ? q.x : (dim == 1 ? q.y : q.z);
-  const float da = qd - sa, db = qd - sb;
-  const bool right = da > 0.f;
-  return {right, fmaxf(right ? fminf(da, db) : -fmaxf(da, db), 0.f)};
-}
-// Pipelined state of the split-key walk: the split key of node c1 (loaded by
-// the previous step) and the previous step's point record, to be tested now.
-struct SkState {
-  uint32_t sk;
-  float4 pp;
-  bool pend;
-};
-
-// lean_step on split keys (same transitions, JUMP, queue and box skip).
-template <int K, bool WIDE, bool BOX = false>
-__device__ __forceinline__ void lean_step_sk(const float4* __restrict__ nodes, const uint32_t* __restrict__ skeys,
-                                             uint32_t n, v3 q, double tail, LeanWalk& w, SkState& st, double* lq,
-                                             int lstride, BoxView bx = {}, float4* ba = nullptr,
-                                             float4* bb = nullptr) {
-  const SkPlane pl = sk_plane(st.sk, q);
-  const bool within = pl.gap * pl.gap <= w.bound;
-  const bool skip = BOX && !w.up && w.c1 <= bx.nbox && box_d2(*ba, *bb, q) > w.bound;
-  const uint32_t close1 = 2 * w.c1 + (pl.right ? 1u : 0u), far1 = close1 ^ 1u;
-  const bool closeok = close1 <= n;
-  const bool test = !skip && (w.up || !closeok);
-  const bool descend = !skip && !w.up && closeok;
-  const bool farok = !skip && !descend && far1 <= n && within;
-  const bool stay = descend || farok;
-  const uint32_t next = descend ? close1 : (farok ? far1 : w.upnode);
-  const bool go = w.walking && (stay || w.upnode != 0);
-  const uint32_t c1n = go ? next : w.c1;
-  const uint32_t skn = skey1<WIDE>(skeys, c1n);   // the chain: issued first
-  if (BOX && c1n <= bx.nbox) {
-    const float4* bp = box1<WIDE>(bx.box, c1n);
-    *ba = bp[0];
-    *bb = bp[1];
-  }
-  // nothing below moves above the descent's load (the point test waits for
-  // the previous step's record)
-  __builtin_amdgcn_sched_barrier(0);
-  // the previous step's point test (unpacked subtractions: a v_pk_add on
-  // (y, z) made the compiler copy the loaded record into an aligned pair at the
-  // loop head, i.e. wait for the record before the descent)
-  {
-    const float dx = fsub_v(q.x, st.pp.x), dy = fsub_v(q.y, st.pp.y), dz = fsub_v(q.z, st.pp.z);
-    const float d2 = dx * dx + dy * dy + dz * dz;
-    const double key = gkey(d2, __float_as_uint(st.pp.w));
-    const bool cand = st.pend && key < tail;
-    lq[(w.qn + 1) * lstride] = key;
-    w.qn += cand ? 1 : 0;
-  }
-  // this node's point record, only when its plane gap is within the bound; the
-  // load is issued by every lane (the others read the root's record, one line
-  // for the wave), so the loop keeps one known load in flight: a conditional
-  // load made every wait a vmcnt(0), the descent's included
-  const bool need = w.walking && test && within;
-  st.pp = node1<WIDE>(nodes, need ? w.c1 : 1u);
-  st.pend = need;
-  w.far_mask = stay ? (w.far_mask << 1 | (farok ? 1u : 0u)) : w.far_mask >> w.j1;
-  w.up = !stay;
-  w.c1 = c1n;
-  w.walking = go;
-  w.set_jump();
-  st.sk = skn;
-}
-
 // Wave-uniform insert round: every lane pops one queued key (an empty queue
 // reads slot 0, DBL_MAX); list_insert leaves the list unchanged for a key above
 // its last entry, so the round needs no per-lane branch.
@@ -514,21 +394,18 @@ __device__ __forceinline__ void lean_round(double (&list)[K], LeanWalk& w, const
 // walks and queues are done (returns true) or the wave has run `limit`
 // iterations (false). BUDGET > 0: at BUDGET iterations the lanes still walking
 // stop and are reported through `aborted`; their lists are incomplete.
-template <int K, int QL, bool WIDE, int BUDGET, bool BOX, bool SK = false>
+template <int K, int QL, bool WIDE, int BUDGET, bool BOX>
 __device__ __forceinline__ bool lean_phase(const float4* __restrict__ nodes, uint32_t n, v3 q, double (&list)[K],
                                            double* lq, int lstride, BoxView bx, LeanWalk& w, float4& nd, float4& ba,
-                                           float4& bb, int& it, int limit, bool& aborted,
-                                           const uint32_t* __restrict__ skeys = nullptr, SkState* st = nullptr) {
+                                           float4& bb, int& it, int limit, bool& aborted) {
   for (;;) {
-    if (SK) lean_step_sk<K, WIDE, BOX>(nodes, skeys, n, q, list[K - 1], w, *st, lq, lstride, bx, &ba, &bb);
-    else lean_step<K, WIDE, BOX>(nodes, n, q, list[K - 1], w, nd, lq, lstride, bx, &ba, &bb);
+    lean_step<K, WIDE, BOX>(nodes, n, q, list[K - 1], w, nd, lq, lstride, bx, &ba, &bb);
     ++it;
     if (BUDGET > 0 && it == BUDGET) {
       aborted = w.walking;
       w.walking = false;
     }
-    // a split-key lane's last point test is still pending one step after its walk ends
-    const bool any_walking = ballot(w.walking || (SK && st->pend)) != 0;
+    const bool any_walking = ballot(w.walking) != 0;
     if (ballot(w.qn == QL) != 0 || !any_walking) {   // wave-uniform insert round
       lean_round<K>(list, w, lq, lstride);
       if (!any_walking && ballot(w.qn > 0) == 0) return true;
@@ -542,10 +419,10 @@ __device__ __forceinline__ bool lean_phase(const float4* __restrict__ nodes, uin
 // cost ~14 VALU and a 32-B load per step, which the short walks of a dense map
 // do not pay back; the long ones -- a wave that wanders along planar walls or
 // a thin shell of a far patch -- are cut short by them.
-template <int K, int QL, bool WIDE, int BUDGET = 0, int BOXAFTER = -1, bool SK = false>
+template <int K, int QL, bool WIDE, int BUDGET = 0, int BOXAFTER = -1>
 __device__ __forceinline__ bool knn_walk_lean(const float4* __restrict__ nodes, int n, v3 q, float cut, bool valid,
                                               double (&list)[K], double* lq, int lstride, BoxView bx = {},
-                                              int* it_out = nullptr, const uint32_t* __restrict__ skeys = nullptr) {
+                                              int* it_out = nullptr) {
   const double sentinel = gkey(cut, kNoWord);
 #pragma unroll
   for (int j = 0; j < K; j++) list[j] = sentinel;
@@ -554,30 +431,22 @@ __device__ __forceinline__ bool knn_walk_lean(const float4* __restrict__ nodes, 
   w.start(cut, valid);
   w.qn = 0;
   lq[0] = __longlong_as_double(0x7FEFFFFFFFFFFFFFll);   // slot 0: DBL_MAX, never inserted
-  float4 nd = {};
-  SkState st;
-  if (SK) {
-    st.sk = skey1<WIDE>(skeys, 1);
-    st.pp = make_float4(0.f, 0.f, 0.f, 0.f);
-    st.pend = false;
-  } else {
-    nd = node1<WIDE>(nodes, 1);
-  }
+  float4 nd = node1<WIDE>(nodes, 1);
   float4 ba = {}, bb = {};
   bool aborted = false;
   int it = 0;   // wave-uniform
   bool done = false;
   if (BOXAFTER != 0)
-    done = lean_phase<K, QL, WIDE, BUDGET, false, SK>(nodes, (uint32_t)n, q, list, lq, lstride, bx, w, nd, ba, bb,
-                                                      it, BOXAFTER, aborted, skeys, &st);
+    done = lean_phase<K, QL, WIDE, BUDGET, false>(nodes, (uint32_t)n, q, list, lq, lstride, bx, w, nd, ba, bb, it,
+                                                  BOXAFTER, aborted);
   if (BOXAFTER >= 0 && !done) {
     if (w.c1 <= bx.nbox) {   // the current node's box (the skip test reads it next step)
       const float4* bp = box1<WIDE>(bx.box, w.c1);
       ba = bp[0];
       bb = bp[1];
     }
-    lean_phase<K, QL, WIDE, BUDGET, true, SK>(nodes, (uint32_t)n, q, list, lq, lstride, bx, w, nd, ba, bb, it, -1,
-                                              aborted, skeys, &st);
+    lean_phase<K, QL, WIDE, BUDGET, true>(nodes, (uint32_t)n, q, list, lq, lstride, bx, w, nd, ba, bb, it, -1,
+                                          aborted);
   }
   if (it_out) *it_out = it;
   return aborted;
@@ -797,26 +666,17 @@ __device__ __forceinline__ float follower_cut(const float4* __restrict__ lead, i
 // leader launch (231k queries) took 16.8 ms.
 constexpr int kSubtreeLevels = 6;   // 63 nodes
 constexpr int kSubtreeTop = (1 << kSubtreeLevels) - 1 - (kKNearest - 1);   // 14: rank 50 of 63 from the top
-// (any subtree's 63 points bound it: with split keys the descent reads 4 B per
-// level and may pick the other side within 3 ulp of a plane)
 template <bool WIDE>
-__device__ __forceinline__ float subtree_cut(const float4* __restrict__ nodes, uint32_t n, v3 q, float plain,
-                                             const uint32_t* __restrict__ skeys = nullptr) {
+__device__ __forceinline__ float subtree_cut(const float4* __restrict__ nodes, uint32_t n, v3 q, float plain) {
   const int D = 31 - __clz(n);   // deepest level (0-based): levels 0 .. D - 1 are complete
   const int dz = D - kSubtreeLevels;
   if (dz < 0) return plain;
   uint32_t c1 = 1;
   for (int d = 0; d < dz; d++) {   // close path
-    bool right;
-    if (skeys) {
-      right = sk_plane(skey1<WIDE>(skeys, c1), q).right;
-    } else {
-      const float4 nd = node1<WIDE>(nodes, c1);
-      const uint32_t dim = __float_as_uint(nd.w) & 3u;
-      const float diff = dim == 0 ? q.x - nd.x : (dim == 1 ? q.y - nd.y : q.z - nd.z);
-      right = diff > 0.f;
-    }
-    c1 = 2 * c1 + (right ? 1u : 0u);
+    const float4 nd = node1<WIDE>(nodes, c1);
+    const uint32_t dim = __float_as_uint(nd.w) & 3u;
+    const float diff = dim == 0 ? q.x - nd.x : (dim == 1 ? q.y - nd.y : q.z - nd.z);
+    c1 = 2 * c1 + (diff > 0.f ? 1u : 0u);
   }
   float top[kSubtreeTop];   // descending
 #pragma unroll
@@ -846,8 +706,7 @@ template <int TAG, bool LEADERS, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && (kGatherBox == 1 || kGatherBox == 2) ? 3 : 4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
-    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx, int64_t t1,
-    const uint32_t* __restrict__ skeys) {
+    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx, int64_t t1) {
   // lanes [0, t1): leader index (rank t S) or follower index
   __shared__ double lq[(kGatherQL + 1) * 256];
   const float R2 = kKMaxDistance * kKMaxDistance;
@@ -875,7 +734,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
   float cut = lean_cut(R2);
   if (valid) {
     if (LEADERS || redo_lane) {
-      cut = subtree_cut<WIDE>(nodes, (uint32_t)n, q, cut, skeys);
+      cut = subtree_cut<WIDE>(nodes, (uint32_t)n, q, cut);
       // a retried leader whose list was full when its budget ran out recorded
       // that list's last d^2: its 50 points lie within it, so it bounds the
       // 50th nearest (and admits it: only d^2 <= cut are candidates)
@@ -890,16 +749,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
   double list[kKNearest];
   bool aborted;
   int* const itp = nullptr;
-  constexpr bool SK = PM_GATHER_SKEY;
   if (kGatherBox == 2 || (kGatherBox == 1 && LEADERS) || (kGatherBox == 3 && !LEADERS)) {
-    aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0, kBoxAfter, SK>(
-        nodes, n, q, cut, valid, list, lq + threadIdx.x, 256, bx, itp, skeys);
+    aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0, kBoxAfter>(
+        nodes, n, q, cut, valid, list, lq + threadIdx.x, 256, bx, itp);
   } else if (kGatherBox == 1 && redo_lane) {   // block-uniform: the retried leaders
-    aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, 0, kBoxAfter, SK>(nodes, n, q, cut, valid, list,
-                                                                          lq + threadIdx.x, 256, bx, itp, skeys);
+    aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, 0, kBoxAfter>(nodes, n, q, cut, valid, list,
+                                                                      lq + threadIdx.x, 256, bx, itp);
   } else {
-    aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0, -1, SK>(
-        nodes, n, q, cut, valid, list, lq + threadIdx.x, 256, {}, itp, skeys);
+    aborted = knn_walk_lean<kKNearest, kGatherQL, WIDE, LEADERS ? kLeaderBudget : 0>(nodes, n, q, cut, valid, list,
+                                                                                     lq + threadIdx.x, 256, {}, itp);
   }
   if (valid && !aborted) {
     const bool full = gkey_word(list[kKNearest - 1]) != kNoWord;
@@ -1003,16 +861,6 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   return hipGetLastError();
 #else
   const int64_t nl = Seeds<kSeedGroup>::count(nq);   // leaders: walk ranks 0, S, 2S, ... (G = 1)
-  // split keys: built per call on s before the leader launch (config 3: 727 MB
-  // read, 182 MB written, ~0.15 ms)
-  DevBuf<uint32_t> skey(PM_GATHER_SKEY ? std::max<int64_t>(n, 1) : 0);
-  if (PM_GATHER_SKEY) {
-    if (!skey.p) return hipErrorOutOfMemory;
-    if (n > 0) {
-      k_split_keys<<<grid_for(n, 256), 256, 0, s>>>(m->nodes.p, n, skey.p);
-      PM_HIP_TRY(hipGetLastError());
-    }
-  }
   DevBuf<float4> lead(nl);
   DevBuf<uint32_t> retry(kLeaderBudget > 0 ? nl : 0), nretry(kLeaderBudget > 0 ? 1 : 0);
   if (!lead.p || (kLeaderBudget > 0 && (!retry.p || !nretry.p))) return hipErrorOutOfMemory;
@@ -1086,13 +934,13 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
     if (grid <= 0) return hipSuccess;
     const float4 *nd = m->nodes.p, *pl = m->payload.p;
     if (tag == 1 && wide)
-      k_gather_level<1, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, skey.p);
+      k_gather_level<1, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     else if (tag == 1)
-      k_gather_level<1, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, skey.p);
+      k_gather_level<1, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     else if (wide)
-      k_gather_level<0, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, skey.p);
+      k_gather_level<0, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     else
-      k_gather_level<0, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, skey.p);
+      k_gather_level<0, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     return hipGetLastError();
   };
   // leaders (walk ranks 0, S, 2S, ...), then the followers with the retry
