@@ -96,6 +96,7 @@ def _load():
         "orc_trace_photon_range": (C.c_int, [_P, C.POINTER(Light), C.c_int32, C.POINTER(TraceParams), C.c_int64,
                                              C.c_int64, C.c_int32, _P, C.c_int64, C.POINTER(C.c_int64)]),
         "orc_map_create": (C.c_int, [_P, C.c_int64, C.c_float, _P, C.c_int64, C.c_float, C.POINTER(_P)]),
+        "orc_map_set_spec": (C.c_int, [_P, C.c_int32, C.c_int32]),
         "orc_map_destroy": (None, [_P]),
         "orc_set_build_threads": (None, [C.c_int32]),
         "orc_kd_left_balanced": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int32, _P]),
@@ -230,6 +231,15 @@ class PhotonMap:
                                 b.ctypes.data if len(b) else None, len(b), float(pb), C.byref(h)), "map_create")
         self.h = h
         self.n = len(a) + len(b)
+
+    # alternative specifications of the gather (orc_map_set_spec; a measured
+    # bound on the unpinned choices, not the parity spec): HEAP is required
+    SPEC_DOMAIN_DIM, SPEC_HEAP, SPEC_FMA = 1, 2, 4
+
+    def set_spec(self, flags: int, nthreads: int = 8):
+        """Later gathers / renders through this map follow specification
+        `flags` (0: production, sorted (d^2, original index) lists)."""
+        _chk(lib.orc_map_set_spec(self.h, int(flags), int(nthreads)), "map_set_spec")
 
     def knn(self, q: np.ndarray, k=50, radius=100.0, nthreads=8):
         q = np.ascontiguousarray(q, np.float32)

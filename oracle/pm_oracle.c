@@ -688,6 +688,7 @@ struct orc_map {
   float* pw;       /* n   */
   int32_t* idx;    /* kd order -> original index */
   int32_t* node_lo; int32_t* node_hi; int8_t* node_dim; float* node_split; int32_t nnodes;
+  struct orc_refkd* ref;   /* orc_map_set_spec: the alternative specification, or NULL */
 };
 
 /* ray-tracer/src/hostCode.cu:54-83 loadPhotons: map = a (power_a) ++ b (power_b).
@@ -792,8 +793,10 @@ int orc_map_create(const pm_photon* a, int64_t na, float power_a,
   *out = m;
   return PM_OK;
 }
+static void refkd_destroy(struct orc_refkd* r);
 void orc_map_destroy(orc_map* m) {
   if (!m) return;
+  refkd_destroy(m->ref);
   free(m->pos); free(m->col); free(m->pw); free(m->idx);
   free(m->node_lo); free(m->node_hi); free(m->node_dim); free(m->node_split);
   free(m);
@@ -1016,7 +1019,9 @@ int orc_knn(const orc_map* m, const pm_float3* q, int64_t nq, int32_t k, float m
 
 /* shading.h:93-121 gatherPhotons; sum in (d^2, id) order. k = K_NEAREST is the
  * reference's; config 5 gathers caustics over k = 200. */
+static v3 gather_ref(const orc_map* m, v3 hit, float brdf, int k);
 static v3 gather_one_k(const orc_map* m, v3 hit, float brdf, int k, cand* buf) {
+  if (m->ref) return gather_ref(m, hit, brdf, k);
   float q[3] = {hit.x, hit.y, hit.z};
   const float r2 = knn_one(m, q, k, K_MAX_DISTANCE, buf);
   v3 flux = V3(0.f, 0.f, 0.f);
@@ -1051,6 +1056,229 @@ int orc_gather_k(const orc_map* m, const pm_float3* pts, const float* brdf, int6
 int orc_gather(const orc_map* m, const pm_float3* pts, const float* brdf, int64_t nq,
                int32_t nthreads, pm_float3* out) {
   return orc_gather_k(m, pts, brdf, nq, K_NEAREST, nthreads, out);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Alternative specifications (orc_map_set_spec): what the reference could do
+ * where this build's spec had to choose, restated so that
+ * their effect on the image can be measured (tests/test_spec_bounds.py). NOT
+ * the product's spec and not a parity target: a bound on the unpinned choices.
+ * cudaKDTree is an empty submodule in the reference; what follows restates its
+ * published algorithm as the reference calls it:
+ *   - tree: cukd::buildTree<Photon, Photon_traits> (ray-tracer/src/hostCode.cu:
+ *     85-95), the in-place left-balanced layout of orc_kd_left_balanced, the
+ *     photons reordered into tree order (the reference gathers from that array);
+ *     ORC_SPEC_DOMAIN_DIM: each node's split dimension is the widest extent of
+ *     its DOMAIN box -- the world bounds of all points (the buildTree output the
+ *     reference passes as globalPhotonsBounds), clipped at every ancestor's split
+ *     plane (left child: upper = the split coordinate, right: lower = it) --
+ *     instead of the extent of the subtree's own points;
+ *   - kNN (ORC_SPEC_HEAP, required): cukd::stackBased::knn with a
+ *     HeapCandidateList<k> (shading.h:11-18): a pre-order walk (test the node's
+ *     point, push the far child when its plane distance^2 < the cull distance,
+ *     descend to the close child; pop entries not culled), candidates kept as
+ *     64-bit (d^2 bits << 32 | TREE index) in a max-heap initialised to
+ *     (max_radius^2, -1) (replace the root, sift down); a candidate enters when
+ *     its key is below the heap's root;
+ *   - gatherPhotons (shading.h:93-121) over the heap ARRAY order, ids being tree
+ *     indices into the reordered photons (the `id > num_photons` test kept);
+ *   - ORC_SPEC_FMA: nvcc's default contraction (-fmad=true): the squared
+ *     distances as fma(z, z, fma(y, y, x * x)), the cone weight as
+ *     fma(-dist / r, C, 1) and the flux sum as fma(s, colour, flux). */
+#define ORC_SPEC_DOMAIN_DIM 1
+#define ORC_SPEC_HEAP 2
+#define ORC_SPEC_FMA 4
+struct orc_refkd {
+  int flags;
+  int64_t n;
+  float* pos; float* col; float* pw;   /* tree order */
+  int8_t* dim;
+};
+static void refkd_destroy(struct orc_refkd* r) {
+  if (!r) return;
+  free(r->pos); free(r->col); free(r->pw); free(r->dim);
+  free(r);
+}
+/* lb_build with the split dimension taken from the node's domain box */
+typedef struct { lb_elem* e; int32_t* tags; int64_t t, lo, hi; float blo[3], bhi[3]; int par; } lbd_task;
+static void lbd_build(lb_elem* e, int32_t* tags, int64_t t, int64_t lo, int64_t hi, const float blo_in[3],
+                      const float bhi_in[3], int par);
+static void* lbd_thread(void* arg) {
+  lbd_task* k = (lbd_task*)arg;
+  lbd_build(k->e, k->tags, k->t, k->lo, k->hi, k->blo, k->bhi, k->par);
+  return NULL;
+}
+static void lbd_build(lb_elem* e, int32_t* tags, int64_t t, int64_t lo, int64_t hi, const float blo_in[3],
+                      const float bhi_in[3], int par) {
+  float blo[3] = {blo_in[0], blo_in[1], blo_in[2]}, bhi[3] = {bhi_in[0], bhi_in[1], bhi_in[2]};
+  for (;;) {
+    const int64_t s = hi - lo;
+    if (s <= 0) return;
+    int dim = 0;   /* arg_max of the box size, first on a tie */
+    for (int d = 1; d < 3; d++)
+      if (bhi[d] - blo[d] > bhi[dim] - blo[dim]) dim = d;
+    const int64_t ls = orc_left_size(s);
+    lb_select(&e[lo], s, ls, dim);
+    tags[t] = (int32_t)((uint32_t)e[lo + ls].id << 2 | (uint32_t)dim);
+    const float split = lb_unkey(e[lo + ls].k[dim]);
+    float lhi[3] = {bhi[0], bhi[1], bhi[2]};
+    lhi[dim] = split;
+    if (par > 1 && s > 65536) {
+      lbd_task k = {e, tags, 2 * t + 1, lo, lo + ls, {blo[0], blo[1], blo[2]}, {lhi[0], lhi[1], lhi[2]}, par / 2};
+      pthread_t th;
+      if (pthread_create(&th, NULL, lbd_thread, &k) == 0) {
+        float rlo[3] = {blo[0], blo[1], blo[2]};
+        rlo[dim] = split;
+        lbd_build(e, tags, 2 * t + 2, lo + ls + 1, hi, rlo, bhi, par - par / 2);
+        pthread_join(th, NULL);
+        return;
+      }
+    }
+    lbd_build(e, tags, 2 * t + 1, lo, lo + ls, blo, lhi, 1);
+    blo[dim] = split;   /* right subtree: iterate */
+    t = 2 * t + 2;
+    lo = lo + ls + 1;
+  }
+}
+
+int orc_map_set_spec(orc_map* m, int32_t flags, int32_t nthreads) {
+  if (!m || (flags & ~7) || (flags && !(flags & ORC_SPEC_HEAP)) || m->n >= ((int64_t)1 << 30)) return PM_ERR_INVALID;
+  refkd_destroy(m->ref);
+  m->ref = NULL;
+  if (!flags) return PM_OK;
+  const int64_t n = m->n;
+  struct orc_refkd* r = (struct orc_refkd*)calloc(1, sizeof(*r));
+  r->flags = flags;
+  r->n = n;
+  r->pos = (float*)malloc(sizeof(float) * 3 * (size_t)(n + 1));
+  r->col = (float*)malloc(sizeof(float) * 3 * (size_t)(n + 1));
+  r->pw = (float*)malloc(sizeof(float) * (size_t)(n + 1));
+  r->dim = (int8_t*)malloc((size_t)(n + 1));
+  int32_t* tags = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1));
+  const int par = nthreads < 1 ? 1 : (nthreads > 256 ? 256 : nthreads);
+  if (!(flags & ORC_SPEC_DOMAIN_DIM)) {
+    orc_kd_left_balanced(m->pos, 3, n, par, tags);
+  } else if (n > 0) {
+    lb_elem* e = (lb_elem*)malloc(sizeof(lb_elem) * (size_t)n);
+    float blo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, bhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int64_t i = 0; i < n; i++) {
+      for (int d = 0; d < 3; d++) {
+        const float c = m->pos[i * 3 + d];
+        e[i].k[d] = lb_key(c);
+        blo[d] = fminf(blo[d], c);
+        bhi[d] = fmaxf(bhi[d], c);
+      }
+      e[i].id = (int32_t)i;
+    }
+    lbd_build(e, tags, 0, 0, n, blo, bhi, par);
+    free(e);
+  }
+  for (int64_t t = 0; t < n; t++) {
+    const int64_t o = (uint32_t)tags[t] >> 2;
+    for (int d = 0; d < 3; d++) {
+      r->pos[t * 3 + d] = m->pos[o * 3 + d];
+      r->col[t * 3 + d] = m->col[o * 3 + d];
+    }
+    r->pw[t] = m->pw[o];
+    r->dim[t] = (int8_t)(tags[t] & 3);
+  }
+  free(tags);
+  m->ref = r;
+  return PM_OK;
+}
+
+static inline uint64_t hc_encode(float d2, int32_t id) {
+  uint32_t u;
+  memcpy(&u, &d2, 4);
+  return (uint64_t)u << 32 | (uint32_t)id;
+}
+static inline float hc_d2(uint64_t e) {
+  const uint32_t u = (uint32_t)(e >> 32);
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+/* HeapCandidateList<k>::push: replace the root, sift down; returns maxRadius2 */
+static float hc_push(uint64_t* h, int k, float d2, int32_t id) {
+  const uint64_t e = hc_encode(d2, id);
+  if (e >= h[0]) return hc_d2(h[0]);
+  int pos = 0;
+  for (;;) {
+    const int c1 = 2 * pos + 1, c2 = c1 + 1;
+    int big = k;
+    uint64_t bv = 0;
+    if (c1 < k) { big = c1; bv = h[c1]; }
+    if (c2 < k && h[c2] > bv) { big = c2; bv = h[c2]; }
+    if (big == k || bv < e) { h[pos] = e; break; }
+    h[pos] = bv;
+    pos = big;
+  }
+  return hc_d2(h[0]);
+}
+static inline float ref_d2(const float* p, const float q[3], int fma_on) {
+  const float dx = p[0] - q[0], dy = p[1] - q[1], dz = p[2] - q[2];
+  if (fma_on) return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+  return dx * dx + dy * dy + dz * dz;
+}
+static v3 gather_ref(const orc_map* m, v3 hit, float brdf, int k) {
+  const struct orc_refkd* r = m->ref;
+  const int fm = (r->flags & ORC_SPEC_FMA) != 0;
+  const float q[3] = {hit.x, hit.y, hit.z};
+  uint64_t h[256];
+  const float cut = K_MAX_DISTANCE;
+  for (int i = 0; i < k; i++) h[i] = hc_encode(cut * cut, -1);
+  /* cukd::stackBased::knn */
+  struct { int32_t node; float d2; } stack[64];
+  int sp = 0;
+  float cull = hc_d2(h[0]);
+  int64_t node = 0;
+  const int64_t n = r->n;
+  for (;;) {
+    while (node < n) {
+      const float* p = &r->pos[node * 3];
+      cull = hc_push(h, k, ref_d2(p, q, fm), (int32_t)node);
+      const int dim = r->dim[node];
+      const float diff = q[dim] - p[dim];
+      const int64_t l = 2 * node + 1;
+      const int left_close = q[dim] < p[dim];
+      const int64_t close_c = left_close ? l : l + 1, far_c = left_close ? l + 1 : l;
+      const float pd2 = diff * diff;
+      if (pd2 < cull && far_c < n) {
+        stack[sp].node = (int32_t)far_c;
+        stack[sp].d2 = pd2;
+        sp++;
+      }
+      node = close_c;
+    }
+    int found = 0;
+    while (sp > 0) {
+      sp--;
+      if (stack[sp].d2 >= cull) continue;
+      node = stack[sp].node;
+      found = 1;
+      break;
+    }
+    if (!found) break;
+  }
+  const float r2 = cull;
+  /* gatherPhotons over the heap array */
+  v3 flux = V3(0.f, 0.f, 0.f);
+  for (int i = 0; i < k; i++) {
+    const int32_t id = (int32_t)(uint32_t)h[i];
+    if (id < 0 || id > n) continue;
+    const float* p = &r->pos[(int64_t)id * 3];
+    const float* c = &r->col[(int64_t)id * 3];
+    const float dist = sqrtf(ref_d2(p, q, fm));
+    if (fm) {
+      const float w = fmaf(-(dist / sqrtf(r2)), CONE_FILTER_C, 1.f);
+      const float sc = brdf * r->pw[id] * w;
+      flux = V3(fmaf(sc, c[0], flux.x), fmaf(sc, c[1], flux.y), fmaf(sc, c[2], flux.z));
+    } else {
+      const float w = 1 - (dist / sqrtf(r2) * CONE_FILTER_C);
+      flux = add(flux, smul(brdf * r->pw[id] * w, V3(c[0], c[1], c[2])));
+    }
+  }
+  return divf(flux, (1 - (2.f / 3.f) * (1.f / CONE_FILTER_C)) * 2 * PI_F * r2);
 }
 
 /* ------------------------------------------------------------------------ */

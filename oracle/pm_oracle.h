@@ -71,6 +71,11 @@ void orc_set_build_threads(int32_t n);
 int orc_map_create(const pm_photon* a, int64_t na, float power_a,
                    const pm_photon* b, int64_t nb, float power_b, orc_map** out);
 void orc_map_destroy(orc_map* m);
+/* Alternative specifications of the gather (a bound on this build's unpinned
+ * choices; NOT the parity spec): flags 0 = production; else
+ * ORC_SPEC_HEAP (2, required) | ORC_SPEC_DOMAIN_DIM (1) | ORC_SPEC_FMA (4).
+ * Later gathers and renders through m follow it. */
+int orc_map_set_spec(orc_map* m, int32_t flags, int32_t nthreads);
 int orc_knn(const orc_map* m, const pm_float3* q, int64_t nq, int32_t k,
             float max_radius, int32_t nthreads, int32_t* ids, float* d2, float* maxd2);
 int orc_gather(const orc_map* m, const pm_float3* pts, const float* brdf,

@@ -13,7 +13,9 @@ oracle finishes in seconds.
   - kd layout: both maps' trees node for node against the oracle's
     restatement of cukd's left-balanced layout (tests/kd_layout.py);
   - image: a 48-row band at the frame centre rendered by the oracle over the
-    full maps, L_inf <= 1e-3 and >= 99.9 % of pixels bitwise vs the HIP frame.
+    full maps, L_inf <= 1e-3 and >= 99.9 % of pixels bitwise vs the HIP frame;
+    the same band under the oracle's alternative specifications of the
+    reference's unpinned behaviour (tests/test_spec_bounds.py) within 1e-3 of it.
 The GPU photons the maps are built from are the ones the frame used (their
 bitwise agreement with the oracle is the trace check above and, at reduced
 size, test_gpu_workloads.py)."""
@@ -95,6 +97,21 @@ def _frame_vs_oracle(gs, os_, lights, g, c, caustic_k, W=1920, H=1080):
     assert np.mean(rgba.cpu().numpy().view(np.uint32)[rows] != orgba[rows]) <= 0.001
     assert np.mean(orgb[rows]) > 0.01   # a lit band, not an all-black comparison
     checked["band_exact"] = exact
+    # the same band under the alternative specifications of the reference's
+    # unpinned behaviour (tests/test_spec_bounds.py): heap-order sums over
+    # tree-index ids, domain-box split dimensions, nvcc contraction
+    import test_spec_bounds as sb
+    S = oracle.PhotonMap
+    images = sb.spec_images(os_, lights, om["global"], om["caustic"], W, H,
+                            (S.SPEC_HEAP, S.SPEC_HEAP | S.SPEC_DOMAIN_DIM,
+                             S.SPEC_HEAP | S.SPEC_DOMAIN_DIM | S.SPEC_FMA),
+                            rows=(lo, lo + BAND), caustic_k=caustic_k)
+    assert np.array_equal(_bits(images[0]), _bits(orgb))   # the production spec is the band above
+    bounds = sb.spec_bounds(images, rows)
+    sb.report(f"config{'5' if caustic_k else '3'} band {BAND}x{W}", bounds)
+    for f, (e, _) in bounds.items():
+        assert e <= sb.TOL, (f, e)
+    checked["spec_bounds"] = bounds
     del om
     return st, checked, gm.n, cm.n
 
