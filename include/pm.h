@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PM_ABI_VERSION 5
+#define PM_ABI_VERSION 6
 
 enum pm_status {
   PM_OK = 0,
@@ -191,6 +191,19 @@ int pm_trace_capacity(const pm_light* lights, int32_t num_lights,
 int pm_trace_photons(pm_scene* scene, const pm_light* lights, int32_t num_lights,
                      const pm_trace_params* params, pm_photon* d_out,
                      int64_t capacity, int64_t* count, void* stream);
+
+/* Both photon sets of a frame (runNormal + runCaustics, hostCode.cu:112-138)
+ * in ONE persistent launch: params[0] / params[1] (each its own casted count,
+ * mode and shard) trace into d_out[0] / d_out[1] exactly the photons, order,
+ * counts (count[k]) and PM_ERR_CAPACITY behaviour of two pm_trace_photons
+ * calls. Set 0's photons are taken first, so set 1's fill the tail of its
+ * long paths (the frame passes the diffuse set first, the caustic set second).
+ * Phases: 0 = the trace window (the launch through the last compaction), 1 =
+ * the compactions. Sets whose deposit slots exceed one chunk, or whose
+ * max_depth differ, are traced one after the other (same results). */
+int pm_trace_photon_sets(pm_scene* scene, const pm_light* lights, int32_t num_lights,
+                         const pm_trace_params* params /* [2] */, pm_photon* const* d_out /* [2] */,
+                         const int64_t* capacity /* [2] */, int64_t* count /* [2] */, void* stream);
 
 /* ---- stage 2a: kd-tree (cukd::buildTree, hostCode.cu:94-95) -------------- */
 /* In place: reorders d_photons into a left-balanced implicit kd-tree (children

@@ -462,6 +462,116 @@ int pm_trace_photons(pm_scene* sc, const pm_light* lights, int32_t nl, const pm_
   return over ? PM_ERR_CAPACITY : PM_OK;
 }
 
+// Both photon sets of a frame in ONE launch (runNormal + runCaustics,
+// photon-mapping/src/hostCode.cu:112-138): each set's photons, order and
+// capacity behaviour are exactly those of its own pm_trace_photons call.
+static void light_devs(const pm_light* lights, int nl, std::vector<LightDev>& lh) {
+  lh.resize(nl);
+  for (int i = 0; i < nl; i++) {
+    lh[i].pos = make_float4(lights[i].pos.x, lights[i].pos.y, lights[i].pos.z, 0.f);
+    lh[i].rgb = make_float4(lights[i].rgb.x, lights[i].rgb.y, lights[i].rgb.z,
+                            lights[i].source_type == PM_SQUARE_LIGHT ? 1.f : 0.f);
+    lh[i].nrm = make_float4(lights[i].normal.x, lights[i].normal.y, lights[i].normal.z,
+                            (float)lights[i].side_length);
+  }
+}
+
+int pm_trace_photon_sets(pm_scene* sc, const pm_light* lights, int32_t nl, const pm_trace_params* params,
+                         pm_photon* const* d_out, const int64_t* capacity, int64_t* count, void* stream) {
+  if (!sc || !params || !d_out || !capacity || !count) return PM_ERR_INVALID;
+  count[0] = count[1] = 0;
+  std::vector<int64_t> loff[2];
+  int64_t lo[2], hi[2], np[2];
+  int per[2];
+  for (int k = 0; k < 2; k++) {
+    if (capacity[k] < 0) return PM_ERR_INVALID;
+    const int st = shard_range(lights, nl, &params[k], loff[k], lo[k], hi[k]);
+    if (st != PM_OK) return st;
+    per[k] = params[k].caustics_mode ? 1 : std::max(params[k].max_depth - 1, 0);
+    np[k] = (per[k] > 0 && nl > 0) ? hi[k] - lo[k] : 0;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  AllocStream alloc_scope(s);
+  PM_SAME_DEVICE(alloc_scope, sc);
+  PM_PTR_DEVICE(alloc_scope, d_out[0]);
+  PM_PTR_DEVICE(alloc_scope, d_out[1]);
+  // the deposit slots of both sets within the one-chunk budget (as
+  // pm_trace_photons' ~16 GB), one max_depth; else one call per set
+  const bool one = params[0].max_depth == params[1].max_depth && np[0] + np[1] <= 0xFFFFFFFFll &&
+                   (np[0] * per[0] + np[1] * per[1]) * 40 <= (int64_t)16e9;
+  if (!one) {
+    hipEvent_t a = nullptr, b = nullptr;
+    PM_TRY_ST(hipEventCreate(&a));
+    if (hipEventCreate(&b) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      return PM_ERR_HIP;
+    }
+    (void)hipEventRecord(a, s);
+    double compact = 0.0;
+    int st = PM_OK;
+    for (int k = 0; k < 2 && (st == PM_OK || st == PM_ERR_CAPACITY); k++) {
+      const int sk = pm_trace_photons(sc, lights, nl, &params[k], d_out[k], capacity[k], &count[k], stream);
+      compact += g_phase_us[PH_COMPACT];
+      if (st == PM_OK) st = sk;
+    }
+    (void)hipEventRecord(b, s);
+    float ms = 0.f;
+    if (hipEventSynchronize(b) == hipSuccess && hipEventElapsedTime(&ms, a, b) == hipSuccess) {
+      g_phase_us[PH_TRACE] = (double)ms * 1000.0;
+      g_phase_us[PH_COMPACT] = compact;
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return st;
+  }
+  reset_phase(PH_TRACE);
+  reset_phase(PH_COMPACT);
+  if (np[0] + np[1] == 0) return PM_OK;
+  std::vector<LightDev> lh;
+  light_devs(lights, nl, lh);
+  DevBuf<LightDev> dl(nl);
+  DevBuf<int64_t> dloff0(nl + 1), dloff1(nl + 1);
+  DevBuf<pm_photon> slots0((size_t)np[0] * per[0]), slots1((size_t)np[1] * per[1]);
+  DevBuf<uint32_t> cnt0(np[0]), cnt1(np[1]), off0(np[0]), off1(np[1]), tot(2);
+  if (!dl.p || !dloff0.p || !dloff1.p || (np[0] && (!slots0.p || !cnt0.p || !off0.p)) ||
+      (np[1] && (!slots1.p || !cnt1.p || !off1.p)) || !tot.p)
+    return PM_ERR_OOM;
+  PM_TRY_ST(hipMemcpyAsync(dl.p, lh.data(), sizeof(LightDev) * nl, hipMemcpyHostToDevice, s));
+  PM_TRY_ST(hipMemcpyAsync(dloff0.p, loff[0].data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
+  PM_TRY_ST(hipMemcpyAsync(dloff1.p, loff[1].data(), sizeof(int64_t) * (nl + 1), hipMemcpyHostToDevice, s));
+  PM_TRY_ST(hipMemsetAsync(tot.p, 0, 2 * sizeof(uint32_t), s));
+  const PathSet A{dloff0.p, lo[0], np[0], params[0].caustics_mode ? 1 : 0, slots0.p, cnt0.p};
+  const PathSet B{dloff1.p, lo[1], np[1], params[1].caustics_mode ? 1 : 0, slots1.p, cnt1.p};
+  uint32_t t[2] = {0, 0};
+  bool over[2] = {false, false};
+  {
+    // PH_TRACE: the trace WINDOW, the launch's start to the last compaction's
+    // end (one stream); PH_COMPACT: the scans and compactions alone
+    PhaseTimer win(PH_TRACE, s);
+    PM_TRY_ST(launch_trace_sets(sc, dl.p, nl, A, B, params[0].max_depth, s));
+    PhaseTimer tc(PH_COMPACT, s);
+    if (np[0]) PM_TRY_ST(exclusive_scan_u32(cnt0.p, off0.p, np[0], tot.p, s));
+    if (np[1]) PM_TRY_ST(exclusive_scan_u32(cnt1.p, off1.p, np[1], tot.p + 1, s));
+    PM_TRY_ST(hipMemcpyAsync(t, tot.p, sizeof(t), hipMemcpyDeviceToHost, s));
+    PM_TRY_ST(hipStreamSynchronize(s));
+    const PathSet* sets[2] = {&A, &B};
+    const uint32_t* offs[2] = {off0.p, off1.p};
+    for (int k = 0; k < 2; k++) {
+      if (!np[k]) continue;
+      if ((int64_t)t[k] <= capacity[k] && d_out[k])
+        PM_TRY_ST(launch_compact(sets[k]->slots, sets[k]->cnt, offs[k], np[k], d_out[k], s));
+      else
+        over[k] = true;
+    }
+  }
+  PM_TRY_ST(hipStreamSynchronize(s));
+  count[0] = t[0];
+  count[1] = t[1];
+  const int st = check_overflow(sc, s);
+  if (st != PM_OK) return st;
+  return (over[0] || over[1]) ? PM_ERR_CAPACITY : PM_OK;
+}
+
 // ------------------------------------------------------------------ stage 2
 int pm_kdtree_build(pm_kd_photon* d, int64_t n, pm_box* bounds, void* stream) {
   if (n < 0 || (n > 0 && !d) || n >= kMaxMapPhotons) return PM_ERR_INVALID;

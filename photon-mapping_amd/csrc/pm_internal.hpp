@@ -69,6 +69,20 @@ struct LightDev {
   float4 nrm;
 };
 
+// One photon set of a trace launch (trace.hip): photons [g_lo, g_lo + np) of the
+// set's global index range (per-light offsets loff, device), its mode, and its
+// deposit slots (deposit k of photon i at slots[k * np + i]) and counts.
+struct PathSet {
+  const int64_t* loff = nullptr;
+  int64_t g_lo = 0, np = 0;
+  int caustic = 0;
+  pm_photon* slots = nullptr;
+  uint32_t* cnt = nullptr;
+};
+// Both sets in one launch (B.np may be 0; see launch_trace_fused).
+hipError_t launch_trace_sets(pm_scene* sc, const LightDev* d_lights, int nl, PathSet A, PathSet B, int maxd,
+                             hipStream_t s);
+
 // phase timers (pm_last_phase_us)
 enum Phase { PH_TRACE = 0, PH_COMPACT = 1, PH_KDBUILD = 2, PH_PATHS = 3, PH_GATHER = 4, PH_RESOLVE = 5, PH_BVH = 6,
              PH_GATHER_GLOBAL = 7, PH_COUNT = 8 };

@@ -243,18 +243,18 @@ __global__ __launch_bounds__(kShadeBlock) void k_ph_shade(DevScene S, const Phot
 #define PM_TPATH_BLOCKS 14
 #endif
 __global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TPATH_WAVES) void k_ph_paths(
-    DevScene S, const LightDev* __restrict__ lights, const int64_t* __restrict__ loff, int nl, int64_t g_lo,
-    int64_t np, int maxd, int caustic, pm_photon* __restrict__ slots, uint32_t* __restrict__ cnt,
+    DevScene S, const LightDev* __restrict__ lights, int nl, PathSet A, PathSet B, int maxd,
     unsigned long long* __restrict__ next, int* overflow) {
   __shared__ int stack[kStackDepth * kTBlock];
   int* const st = stack + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int64_t np = A.np + B.np;   // photons [0, A.np) are set A's, the rest set B's
   int spill[kSpillDepth > 0 ? kSpillDepth : 1];
   Ray r;
   HitInfo h{kPhotonTmax, -1, -1};
   int node = 0, sp = 0, b = 0;
-  int64_t pi = -1;      // this lane's photon (-1: idle)
+  int64_t pi = -1;      // this lane's photon (-1: idle), an index over both sets
   bool pend = false;    // its segment's traversal is done, the event not yet run
   uint32_t rng = 0, n = 0;
   v3 color = {0.f, 0.f, 0.f};
@@ -263,9 +263,10 @@ __global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TPATH_WAVES) void k_ph_pa
     const uint64_t pm = __ballot(pend);
     if (pm != 0 && (__popcll(pm) >= PM_PATH_EVENT_MIN || __ballot(pi >= 0 && !pend) == 0)) {
       if (pend) {
+        const bool inb = pi >= A.np;
         v3 so, sd;
-        if (ph_event(S, r.o, r.d, h.t, h.slot, rng, color, n, b, (uint32_t)pi, np, maxd, caustic, slots, cnt, so,
-                     sd)) {
+        if (ph_event(S, r.o, r.d, h.t, h.slot, rng, color, n, b, (uint32_t)(inb ? pi - A.np : pi), inb ? B.np : A.np,
+                     maxd, inb ? B.caustic : A.caustic, inb ? B.slots : A.slots, inb ? B.cnt : A.cnt, so, sd)) {
           ray_prep(r, so, sd);
           h = HitInfo{kPhotonTmax, -1, -1};
           node = 0;
@@ -287,8 +288,9 @@ __global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TPATH_WAVES) void k_ph_pa
       if (pi < 0) {
         const int64_t i = (int64_t)base + __popcll(idle & lt_mask);
         if (i < np) {
+          const bool inb = i >= A.np;
           v3 o, d;
-          ph_emit(lights, loff, nl, g_lo + i, rng, o, d, color);
+          ph_emit(lights, inb ? B.loff : A.loff, nl, inb ? B.g_lo + (i - A.np) : A.g_lo + i, rng, o, d, color);
           ray_prep(r, o, d);
           h = HitInfo{kPhotonTmax, -1, -1};
           node = 0;
@@ -309,19 +311,20 @@ __global__ __launch_bounds__(kTBlock) PM_WAVES_ATTR(PM_TPATH_WAVES) void k_ph_pa
   }
 }
 
-static hipError_t launch_trace_fused(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl,
-                                     int64_t g_lo, int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt,
-                                     hipStream_t s) {
+// One persistent launch over both sets (B.np may be 0): set A's photons are
+// taken first, so set B's (the frame passes the caustic set, whose paths end
+// at their first diffuse hit) fill the tail that A's long paths leave.
+static hipError_t launch_trace_fused(pm_scene* sc, const LightDev* d_lights, int nl, const PathSet& A,
+                                     const PathSet& B, int maxd, hipStream_t s) {
   int cus = 0;   // of the stream's device (a process may drive several)
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, stream_device(s)) != hipSuccess || cus <= 0)
     cus = 256;
   DevBuf<unsigned long long> next(1);
   if (!next.p) return hipErrorOutOfMemory;
   PM_HIP_TRY(hipMemsetAsync(next.p, 0, sizeof(unsigned long long), s));
-  const int64_t want = (np + kTBlock - 1) / kTBlock;
+  const int64_t want = (A.np + B.np + kTBlock - 1) / kTBlock;
   const int grid = (int)std::min<int64_t>(want, (int64_t)cus * PM_TPATH_BLOCKS);
-  k_ph_paths<<<grid, kTBlock, 0, s>>>(sc->view(), d_lights, d_loff, nl, g_lo, np, maxd, caustic, slots, cnt, next.p,
-                                      sc->overflow.p);
+  k_ph_paths<<<grid, kTBlock, 0, s>>>(sc->view(), d_lights, nl, A, B, maxd, next.p, sc->overflow.p);
   PM_HIP_TRY(hipGetLastError());
   return hipStreamSynchronize(s);   // the counter is freed on return
 }
@@ -389,11 +392,29 @@ __global__ __launch_bounds__(256) void k_compact_photons(const pm_photon* slots,
 
 hipError_t launch_trace_chunk(pm_scene* sc, const LightDev* d_lights, const int64_t* d_loff, int nl, int64_t g_lo,
                               int64_t np, int maxd, int caustic, pm_photon* slots, uint32_t* cnt, hipStream_t s) {
-  if (np <= 0) return hipSuccess;
-  if (maxd <= 0) return hipMemsetAsync(cnt, 0, sizeof(uint32_t) * np, s);
-  if (np > 0xFFFFFFFFll) return hipErrorInvalidValue;   // photon ids and live counts are 32-bit
-  if (PM_TRACE_FUSED) return launch_trace_fused(sc, d_lights, d_loff, nl, g_lo, np, maxd, caustic, slots, cnt, s);
-  return launch_trace_wavefront(sc, d_lights, d_loff, nl, g_lo, np, maxd, caustic, slots, cnt, s);
+  return launch_trace_sets(sc, d_lights, nl, PathSet{d_loff, g_lo, np, caustic, slots, cnt}, PathSet{}, maxd, s);
+}
+
+hipError_t launch_trace_sets(pm_scene* sc, const LightDev* d_lights, int nl, PathSet A, PathSet B, int maxd,
+                             hipStream_t s) {
+  if (A.np < 0 || B.np < 0 || A.np + B.np > 0xFFFFFFFFll)   // photon ids and live counts are 32-bit
+    return hipErrorInvalidValue;
+  if (A.np + B.np == 0) return hipSuccess;
+  if (maxd <= 0) {
+    if (A.np > 0) PM_HIP_TRY(hipMemsetAsync(A.cnt, 0, sizeof(uint32_t) * A.np, s));
+    if (B.np > 0) PM_HIP_TRY(hipMemsetAsync(B.cnt, 0, sizeof(uint32_t) * B.np, s));
+    return hipSuccess;
+  }
+  if (PM_TRACE_FUSED) {
+    if (A.np == 0) std::swap(A, B);
+    return launch_trace_fused(sc, d_lights, nl, A, B, maxd, s);
+  }
+  // the wavefront path (check variant): one set after the other
+  for (const PathSet* P : {&A, &B})
+    if (P->np > 0)
+      PM_HIP_TRY(launch_trace_wavefront(sc, d_lights, P->loff, nl, P->g_lo, P->np, maxd, P->caustic, P->slots, P->cnt,
+                                        s));
+  return hipSuccess;
 }
 
 hipError_t launch_compact(const pm_photon* slots, const uint32_t* cnt, const uint32_t* off, int64_t np,

@@ -163,6 +163,8 @@ _SIGNATURES = {
     "pm_trace_capacity": (C.c_int, [C.POINTER(Light), C.c_int32, C.POINTER(TraceParams), C.POINTER(C.c_int64)]),
     "pm_trace_photons": (C.c_int, [_P, C.POINTER(Light), C.c_int32, C.POINTER(TraceParams), _P, C.c_int64,
                                    C.POINTER(C.c_int64), _P]),
+    "pm_trace_photon_sets": (C.c_int, [_P, C.POINTER(Light), C.c_int32, C.POINTER(TraceParams), C.POINTER(_P),
+                                       C.POINTER(C.c_int64), C.POINTER(C.c_int64), _P]),
     "pm_kdtree_build": (C.c_int, [_P, C.c_int64, _P, _P]),
     "pm_photon_map_create": (C.c_int, [_P, C.c_int64, C.c_float, _P, C.c_int64, C.c_float, C.POINTER(_P), _P]),
     "pm_photon_map_create_rows": (C.c_int, [_P, C.c_float, _P, C.c_float, C.POINTER(_P), _P]),
@@ -464,6 +466,31 @@ def run_point_light_ray_gen(scene: Scene, lights, casted: int, max_depth: int, c
     _check(_lib.pm_trace_photons(scene.handle, la, len(lights), C.byref(p), _ptr(buf), buf.shape[0], C.byref(cnt),
                                  _stream(stream)), "pm_trace_photons")
     return buf[: cnt.value]
+
+
+def run_photon_sets(scene: Scene, lights, casted: int, caustic: int, max_depth: int, shard_rank: int = 0,
+                    shard_count: int = 1, out=(None, None), stream=None):
+    """runNormal + runCaustics (photon-mapping/src/hostCode.cu:112-138) in ONE
+    launch (pm_trace_photon_sets): returns (diffuse, caustic) tensors, each
+    exactly run_point_light_ray_gen's output for its set. phase_us("trace") is
+    the trace window (launch through the last compaction), "compact" the
+    compactions."""
+    import torch
+    la = lights_array(lights)
+    ps = (TraceParams * 2)(TraceParams(int(casted), int(max_depth), 0, int(shard_rank), int(shard_count)),
+                           TraceParams(int(caustic), int(max_depth), 1, int(shard_rank), int(shard_count)))
+    bufs = []
+    for k in range(2):
+        cap = C.c_int64()
+        _check(_lib.pm_trace_capacity(la, len(lights), C.byref(ps[k]), C.byref(cap)), "pm_trace_capacity")
+        bufs.append(out[k] if out[k] is not None else
+                    torch.empty((max(1, cap.value), 10), dtype=torch.float32, device="cuda"))
+    ptrs = (_P * 2)(_ptr(bufs[0]), _ptr(bufs[1]))
+    caps = (C.c_int64 * 2)(bufs[0].shape[0], bufs[1].shape[0])
+    cnt = (C.c_int64 * 2)()
+    _check(_lib.pm_trace_photon_sets(scene.handle, la, len(lights), ps, ptrs, caps, cnt, _stream(stream)),
+           "pm_trace_photon_sets")
+    return bufs[0][: cnt[0]], bufs[1][: cnt[1]]
 
 
 def run_normal(scene, lights, casted, max_depth, **kw):

@@ -73,6 +73,13 @@ class FrameConfig:
     # only): for a global trace short enough that the caustic work would
     # otherwise wait behind the render begin
     caustic_after_trace: bool = False
+    # both photon sets in ONE persistent trace launch (pm_trace_photon_sets,
+    # backends with trace_both): the caustic photons fill the diffuse paths'
+    # tail instead of queueing behind the launch on a second stream, and the
+    # trace phase is one stream's window (launch through the last compaction).
+    # One rank: the side thread builds the caustic map after the trace, then
+    # runs pm_render_begin, both beside the global map's kd build
+    one_trace: bool = True
 
 
 def shard_range(total: int, rank: int, world: int):
@@ -395,6 +402,15 @@ class GpuBackend:
                                        cfg.camera["fovy"], cfg.width, cfg.height)
         self.phase = {}
 
+    def trace_both(self, rank: int, world: int):
+        """(diffuse, caustic) photons of this shard in one launch; phase
+        "trace" = the trace window (the launch through the last compaction)."""
+        pm = self.pm
+        g, c = pm.run_photon_sets(self.scene, self.lights, self.cfg.casted, self.cfg.caustic, self.cfg.max_depth,
+                                  shard_rank=rank, shard_count=world, out=(self.gbuf, self.cbuf))
+        self.phase["trace"] = self.phase.get("trace", 0.0) + pm.phase_us("trace")
+        return g, c
+
     def trace(self, caustics: bool, rank: int, world: int):
         pm = self.pm
         casted = self.cfg.caustic if caustics else self.cfg.casted
@@ -434,7 +450,8 @@ class GpuBackend:
         self.phase["kdbuild"] = self.phase.get("kdbuild", 0.0) + kd
         return gm
 
-    def start_render(self, tile_rank: int, tile_count: int, caustic_shard=None, caustic_map: bool = False):
+    def start_render(self, tile_rank: int, tile_count: int, caustic_shard=None, caustic_map: bool = False,
+                     caustic_from_main: bool = False):
         """pm_render_begin on a side stream from a second host thread; returns a
         handle for finish_render. The begin half synchronises its stream before
         it returns, so the job is complete once the thread has ended. With
@@ -447,7 +464,11 @@ class GpuBackend:
         caustic gather stays in finish_render, on a side stream beside the
         global gather's leader launch: run here (pm_render_gather_caustic) it
         landed beside the kd build (config 3: kd 25.3 -> 28 ms, frame
-        unchanged) and, on the Cornell box, held the global gather back."""
+        unchanged) and, on the Cornell box, held the global gather back.
+        caustic_from_main (FrameConfig.one_trace): the main thread traces both
+        sets and hands the caustic photons over with trace_done(pending, c);
+        with caustic_map the thread then builds their map on its stream. With
+        cfg.begin_after_trace, pm_render_begin always waits for trace_done."""
         import threading
         import torch
         pm, c = self.pm, self.cfg
@@ -470,10 +491,17 @@ class GpuBackend:
                     box["r"] = (j, pm.phase_us("paths"))   # phase timers are per host thread
                     return j
 
-                late = c.begin_after_trace and caustic_shard is not None
+                late = c.begin_after_trace
                 if not late:
                     job = begin()
-                if caustic_shard is not None:
+                if caustic_from_main:
+                    box["trace_done"].wait()
+                    if caustic_map and "c_in" in box:
+                        cm = pm.PhotonMap(box["c_in"], pm.CAUSTICS_PHOTON_POWER, stream=side.cuda_stream)
+                        box["cm"] = (cm, pm.phase_us("kdbuild"))
+                    if late:
+                        job = begin()
+                elif caustic_shard is not None:
                     t = pm.run_point_light_ray_gen(self.scene, self.lights, c.caustic, c.max_depth, True,
                                                    shard_rank=caustic_shard[0], shard_count=caustic_shard[1],
                                                    out=self.cbuf, stream=side.cuda_stream)
@@ -487,6 +515,9 @@ class GpuBackend:
                         job = begin()
                     if caustic_map and c.early_caustic_gather:
                         job.gather_caustic(cm, stream=side.cuda_stream)
+                elif late:
+                    box["trace_done"].wait()
+                    job = begin()
             except BaseException as e:   # re-raised by finish_render / join_render
                 box["e"] = e
             finally:
@@ -517,8 +548,11 @@ class GpuBackend:
         return cm
 
     @staticmethod
-    def trace_done(pending):
-        """The global trace is over (begin_after_trace's thread may go on)."""
+    def trace_done(pending, caustic=None):
+        """The global trace is over (begin_after_trace's thread may go on);
+        caustic: the caustic photons, for start_render(caustic_from_main=True)."""
+        if caustic is not None:
+            pending[1]["c_in"] = caustic
         pending[1]["trace_done"].set()
 
     @staticmethod
@@ -561,14 +595,20 @@ def frame(backend, rank: int, world: int, dist=None, rgba=None):
     is that window (HIP events), caustic build included."""
     backend.phase = {}
     pending = None
+    one = getattr(backend.cfg, "one_trace", False) and hasattr(backend, "trace_both")
+    early_caustic = side_caustic = False
     if backend.cfg.overlap_render and hasattr(backend, "start_render"):
-        side_caustic = not (world == 1 and backend.cfg.caustic_after_trace)
-        early_caustic = world == 1 and not backend.cfg.quantize and side_caustic
-        pending = backend.start_render(rank, world, caustic_shard=(rank, world) if side_caustic else None,
-                                       caustic_map=early_caustic)
+        if one:
+            early_caustic = world == 1 and not backend.cfg.quantize
+            pending = backend.start_render(rank, world, caustic_map=early_caustic, caustic_from_main=True)
+        else:
+            side_caustic = not (world == 1 and backend.cfg.caustic_after_trace)
+            early_caustic = world == 1 and not backend.cfg.quantize and side_caustic
+            pending = backend.start_render(rank, world, caustic_shard=(rank, world) if side_caustic else None,
+                                           caustic_map=early_caustic)
     try:
         g, c, gm, cm = _maps(backend, rank, world, dist, pending, pending is not None and early_caustic,
-                             side_caustic=pending is not None and side_caustic)
+                             side_caustic=pending is not None and side_caustic, one_trace=one)
     except BaseException:
         if pending is not None:   # no side work outlives a failed frame
             try:
@@ -606,17 +646,25 @@ def nrows(x) -> int:
     return int(x.n if hasattr(x, "segments") else x.shape[0])
 
 
-def _maps(backend, rank: int, world: int, dist, pending=None, early_caustic: bool = False, side_caustic=None):
-    """Trace both photon sets, exchange them (N > 1), build both maps. With a
-    render pending from start_render(caustic_shard=...) (side_caustic), the
-    caustic photons come from its thread; with early_caustic (world 1), so does
-    the caustic map (returned as None here)."""
-    if side_caustic is None:
-        side_caustic = pending is not None
-    g = backend.trace(False, rank, world)
-    if pending is not None and hasattr(backend, "trace_done"):
-        backend.trace_done(pending)
-    c = backend.caustic_photons(pending) if side_caustic else backend.trace(True, rank, world)
+def _maps(backend, rank: int, world: int, dist, pending=None, early_caustic: bool = False, side_caustic=None,
+          one_trace: bool = False):
+    """Trace both photon sets, exchange them (N > 1), build both maps. one_trace:
+    both sets in one launch (backend.trace_both); with a render pending, its
+    thread is handed the caustic photons and, with early_caustic (world 1),
+    builds their map (returned as None here). Otherwise, with a render pending
+    from start_render(caustic_shard=...) (side_caustic), the caustic photons
+    come from its thread, and with early_caustic so does the caustic map."""
+    if one_trace:
+        g, c = backend.trace_both(rank, world)
+        if pending is not None and hasattr(backend, "trace_done"):
+            backend.trace_done(pending, c)
+    else:
+        if side_caustic is None:
+            side_caustic = pending is not None
+        g = backend.trace(False, rank, world)
+        if pending is not None and hasattr(backend, "trace_done"):
+            backend.trace_done(pending)
+        c = backend.caustic_photons(pending) if side_caustic else backend.trace(True, rank, world)
     if backend.cfg.quantize:   # elementwise: the same before or after the exchange
         g, c = backend.quantize(g), backend.quantize(c)
     sel = None

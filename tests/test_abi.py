@@ -66,7 +66,7 @@ def test_status_strings():
         assert pm_amd.lib.pm_status_string(s) != b"unknown status"
     # 2: pm_render_params.caustic_k; 3: PM_ERR_DEVICE, pm_device_pool_stats; 4: pm_kd_top_sel_*;
     # 5: pm_photon_rows (pm_photon_map_create_rows, pm_kd_shard_plan_create_rows / _from_sel_rows)
-    assert pm_amd.lib.pm_abi_version() == 5
+    assert pm_amd.lib.pm_abi_version() == 6
 
 
 def test_no_cpu_fallback_without_gpu(cornell):

@@ -39,15 +39,26 @@ class _RecordingBackend:
         self._rec("global_map")
         return _Set()
 
+    def trace_both(self, rank, world):
+        self._rec("trace_both")
+        return _Set(), _Set()
+
     # the side thread, as GpuBackend.start_render runs it
-    def start_render(self, tile_rank, tile_count, caustic_shard=None, caustic_map=False):
+    def start_render(self, tile_rank, tile_count, caustic_shard=None, caustic_map=False, caustic_from_main=False):
         box = {"c_ready": threading.Event(), "trace_done": threading.Event()}
-        late = self.cfg.begin_after_trace and caustic_shard is not None
+        late = self.cfg.begin_after_trace
 
         def run():
             if not late:
                 self._rec("render_begin")
-            if caustic_shard is not None:
+            if caustic_from_main:
+                box["trace_done"].wait()
+                if caustic_map and "c_in" in box:
+                    self._rec("side_caustic_map")
+                    box["cm"] = _Set()
+                if late:
+                    self._rec("render_begin")
+            elif caustic_shard is not None:
                 self._rec("side_trace_caustic")
                 box["c"] = _Set()
                 box["c_ready"].set()
@@ -57,6 +68,9 @@ class _RecordingBackend:
                 if late:
                     box["trace_done"].wait()
                     self._rec("render_begin")
+            elif late:
+                box["trace_done"].wait()
+                self._rec("render_begin")
             box["c_ready"].set()
 
         th = threading.Thread(target=run, name="side")
@@ -72,7 +86,9 @@ class _RecordingBackend:
         return pending[1]["cm"]
 
     @staticmethod
-    def trace_done(pending):
+    def trace_done(pending, caustic=None):
+        if caustic is not None:
+            pending[1]["c_in"] = caustic
         pending[1]["trace_done"].set()
 
     @staticmethod
@@ -87,11 +103,16 @@ class _RecordingBackend:
 
 
 @pytest.mark.parametrize("opts,main,side", [
-    ({}, ["trace_global", "global_map", "finish"], ["side_trace_caustic", "side_caustic_map", "render_begin"]),
-    ({"begin_after_trace": False}, ["trace_global", "global_map", "finish"],
+    # default: both sets in one trace launch; the side thread builds the caustic
+    # map and runs the render begin once the trace is over (beside the kd build)
+    ({}, ["trace_both", "global_map", "finish"], ["side_caustic_map", "render_begin"]),
+    ({"begin_after_trace": False}, ["trace_both", "global_map", "finish"], ["render_begin", "side_caustic_map"]),
+    ({"one_trace": False}, ["trace_global", "global_map", "finish"],
+     ["side_trace_caustic", "side_caustic_map", "render_begin"]),
+    ({"one_trace": False, "begin_after_trace": False}, ["trace_global", "global_map", "finish"],
      ["render_begin", "side_trace_caustic", "side_caustic_map"]),
-    ({"caustic_after_trace": True}, ["trace_global", "trace_caustic", "caustic_map", "global_map", "finish"],
-     ["render_begin"]),
+    ({"one_trace": False, "caustic_after_trace": True},
+     ["trace_global", "trace_caustic", "caustic_map", "global_map", "finish"], ["render_begin"]),
 ])
 def test_single_rank_frame_order(opts, main, side):
     from pm_amd import dist
@@ -100,7 +121,9 @@ def test_single_rank_frame_order(opts, main, side):
     dist.frame(be, 0, 1)
     assert [w for w, t in be.log if t != "side"] == main, be.log
     assert [w for w, t in be.log if t == "side"] == side, be.log
-    if cfg.begin_after_trace and not cfg.caustic_after_trace:
-        # the render begin starts only once the global trace is over
+    if cfg.begin_after_trace:
+        # the render begin starts only once the global trace is over, whichever
+        # thread traces the caustic photons (caustic_after_trace too)
         order = [w for w, _ in be.log]
-        assert order.index("render_begin") > order.index("trace_global")
+        first = "trace_both" if cfg.one_trace else "trace_global"
+        assert order.index("render_begin") > order.index(first)

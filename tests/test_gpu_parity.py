@@ -121,6 +121,64 @@ def test_trace_depth_bitwise(cornell, caustics, max_depth):
     assert pg.shape == po.shape and np.array_equal(_bits(pg), _bits(po))
 
 
+@pytest.mark.parametrize("casted,caustic,max_depth,shard", [
+    (20000, 20000, 10, (0, 1)), (30000, 5000, 30, (1, 3)), (20000, 0, 10, (0, 1)), (0, 20000, 10, (0, 1)),
+    (10000, 10000, 1, (0, 1))])
+def test_trace_photon_sets_equal_two_calls(cornell, casted, caustic, max_depth, shard):
+    """pm_trace_photon_sets (both sets in one k_ph_paths launch) gives each set
+    exactly the photons of its own pm_trace_photons call, bitwise; with point
+    and square lights (per-set light offsets differ with the counts)."""
+    import pm_amd
+    meshes, lights = cornell
+    lights = list(lights) + [dict(pos=(0.0, 39.0, 0.0), rgb=(1.0, 0.9, 0.8), power=30.0, normal=(0.0, -1.0, 0.0),
+                                  side=8.0)]
+    gs = pm_amd.Scene(meshes)
+    kw = dict(shard_rank=shard[0], shard_count=shard[1])
+    g, c = pm_amd.run_photon_sets(gs, lights, casted, caustic, max_depth, **kw)
+    window, compact = pm_amd.phase_us("trace"), pm_amd.phase_us("compact")
+    g1 = pm_amd.run_point_light_ray_gen(gs, lights, casted, max_depth, False, **kw)
+    c1 = pm_amd.run_point_light_ray_gen(gs, lights, caustic, max_depth, True, **kw)
+    assert g.shape == g1.shape and c.shape == c1.shape
+    assert np.array_equal(_bits(g.cpu().numpy()), _bits(g1.cpu().numpy()))
+    assert np.array_equal(_bits(c.cpu().numpy()), _bits(c1.cpu().numpy()))
+    if len(g1) + len(c1) > 0:
+        assert window >= compact > 0.0
+
+
+def test_trace_photon_sets_mid_size_full_grid(cornell):
+    """a photon count that fills the persistent grid many times over
+    (2 M + 1 M photons, max_depth 30), so the global-counter drain, the refill at
+    PM_POOL_REFILL idle lanes and the event batching run at full occupancy in the
+    regular suite; each set against its own call and a 1 % shard vs the oracle."""
+    import oracle
+    import pm_amd
+    meshes, lights = cornell
+    gs, os_ = _scene_pair(meshes)
+    g, c = pm_amd.run_photon_sets(gs, lights, 2_000_000, 1_000_000, 30)
+    g1 = pm_amd.run_point_light_ray_gen(gs, lights, 2_000_000, 30, False)
+    c1 = pm_amd.run_point_light_ray_gen(gs, lights, 1_000_000, 30, True)
+    assert np.array_equal(_bits(g.cpu().numpy()), _bits(g1.cpu().numpy()))
+    assert np.array_equal(_bits(c.cpu().numpy()), _bits(c1.cpu().numpy()))
+    for caustics, casted in ((False, 2_000_000), (True, 1_000_000)):
+        pg = pm_amd.run_point_light_ray_gen(gs, lights, casted, 30, caustics, shard_rank=57, shard_count=100)
+        po = oracle.trace(os_, lights, casted, 30, caustics, shard_rank=57, shard_count=100,
+                          nthreads=conftest.ORACLE_THREADS)
+        assert np.array_equal(_bits(pg.cpu().numpy()), _bits(po))
+
+
+def test_trace_photon_sets_capacity(cornell):
+    import pm_amd
+    meshes, lights = cornell
+    gs = pm_amd.Scene(meshes)
+    small = torch.empty((10, 10), dtype=torch.float32, device="cuda")
+    with pytest.raises(pm_amd.PMError) as e:
+        pm_amd.run_photon_sets(gs, lights, 10000, 10000, 10, out=(small, None))
+    assert e.value.status == pm_amd.PM_ERR_CAPACITY
+    with pytest.raises(pm_amd.PMError) as e:
+        pm_amd.run_photon_sets(gs, lights, 10000, 10000, 10, out=(None, small))
+    assert e.value.status == pm_amd.PM_ERR_CAPACITY
+
+
 def test_trace_shards_concatenate(cornell):
     import pm_amd
     meshes, lights = cornell

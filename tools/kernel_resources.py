@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-kernel VGPRs / scratch / LDS / occupancy from hipcc -save-temps device
 assembly (gfx950): python3 tools/kernel_resources.py DIR [--scratch-only]
-(DIR holds *-hip-amdgcn-amd-amdhsa-gfx950.s; see tools/asm_resources.sh)."""
+(DIR holds *-hip-amdgcn-amd-amdhsa-gfx950.s: cd DIR && hipcc <the Makefile's
+HIPFLAGS> -save-temps -c photon-mapping_amd/csrc/X.hip)."""
 import glob, re, sys
 only = "--scratch-only" in sys.argv
 for f in sorted(glob.glob(sys.argv[1] + "/*-hip-amdgcn-amd-amdhsa-gfx950.s")):
