@@ -12,7 +12,7 @@ switches every gather walk to subtree-box skips after one iteration
 reach), so the box path runs on all of them, addresses kd nodes with 64
 bits (PM_FORCE_WIDE=1; production: maps of >= 2^28 nodes only), and builds
 every kd-tree with the selection build (PM_KD_SEL_MIN=0; production: maps of
->= 2^24 elements, the presorted build below), and keeps only 4 traversal-stack
+>= 2^22 elements, the presorted build below), and keeps only 4 traversal-stack
 entries in LDS (PM_STACK_DEPTH=4: the fused photon-path kernel and the render's
 ray pools spill to scratch on the deep-stack scene; the check variant, which
 also has a 4-entry stack, traces photons with the per-bounce wavefront path), so its trees of these small
