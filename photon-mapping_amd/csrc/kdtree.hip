@@ -700,6 +700,91 @@ __device__ __forceinline__ void block_bitonic3(uint64_t (&k)[3], int (&v)[3], in
   }
 }
 
+// The wave levels of a local finish: sub-segment j of local level KB (<= 63
+// elements, positions b0 .. b0 + sz0 - 1) is finished by wave j with shuffles,
+// a packed wave scan and ds_permute (no block barriers, no LDS). e[d]: this
+// lane's element in list d (the sub-segment sorted by (coordinate d, index));
+// nodes go to stage[] by local heap index. (The lists come by value: an array
+// parameter let the callee's selects of e[dim] become loads through a selected
+// address, which kept e[] in scratch once inlined.)
+__device__ __forceinline__ void local_wave_levels(float4 e0, float4 e1, float4 e2, int lane, int j, int KB, int H,
+                                                  int b0, int sz0, float4* stage) {
+  float4 e[3] = {e0, e1, e2};
+  const bool active = lane < sz0;
+  const int p = b0 + lane;                       // this lane's position (fixed)
+  int b = b0, sz = sz0;                          // this lane's segment
+  int lnode = (1 << KB) - 1 + j;                // local heap index of this lane's segment
+  bool placed = !active;
+  for (int k = KB; k < H && sz0 > 0; k++) {
+    const int ls = placed ? 0 : left_size(sz);
+    // segment extents and median from the lanes holding them (all lanes shuffle)
+    const int lf = placed ? lane : b - b0, ll = placed ? lane : b + sz - 1 - b0;
+    float ext[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const float c = coord_of(e[d], d);
+      ext[d] = __shfl(c, ll) - __shfl(c, lf);
+    }
+    int dim = 0;
+    if (ext[1] > ext[dim]) dim = 1;
+    if (ext[2] > ext[dim]) dim = 2;
+    // per component: a select of whole float4s indexed e[] dynamically,
+    // which kept e[] in scratch for the whole wave phase
+    const bool d0 = dim == 0, d1 = dim == 1;
+    const float4 sel = make_float4(d0 ? e[0].x : (d1 ? e[1].x : e[2].x), d0 ? e[0].y : (d1 ? e[1].y : e[2].y),
+                                   d0 ? e[0].z : (d1 ? e[1].z : e[2].z), d0 ? e[0].w : (d1 ? e[1].w : e[2].w));
+    const int lm = placed ? lane : b + ls - b0;
+    const float4 m = make_float4(__shfl(sel.x, lm), __shfl(sel.y, lm), __shfl(sel.z, lm), __shfl(sel.w, lm));
+    const int nid = __float_as_int(m.w);
+    const float nc = coord_of(m, dim);
+    if (!placed && p == b + ls) stage[lnode] = make_float4(m.x, m.y, m.z, __int_as_float((nid << 2) | dim));
+    if (k + 1 == H) break;
+    // class per list, packed (L, R) counts: list d at bits 14d (L) and 14d + 7 (R)
+    uint8_t c[3];
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      c[d] = placed ? 3 : (uint8_t)kd_class(e[d], dim, nc, nid);
+      cnt |= (uint64_t)(c[d] == 0) << (14 * d) | (uint64_t)(c[d] == 2) << (14 * d + 7);
+    }
+    uint64_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t up = __shfl_up(inc, o);
+      if (lane >= o) inc += up;
+    }
+    const int lb = b - b0 - 1;   // lane before the segment (-1: none)
+    const uint64_t before = __shfl(inc, lb < 0 ? 0 : lb);
+    const uint64_t ex = inc - cnt - (lb < 0 || placed ? 0ull : before);
+    // forward permute of the three elements to their positions in the segment
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      int dst = p;
+      if (c[d] == 0) dst = b + (int)((ex >> (14 * d)) & 127);
+      else if (c[d] == 1) dst = b + ls;
+      else if (c[d] == 2) dst = b + ls + 1 + (int)((ex >> (14 * d + 7)) & 127);
+      const int a = (dst - b0) * 4;
+      e[d].x = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].x)));
+      e[d].y = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].y)));
+      e[d].z = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].z)));
+      e[d].w = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].w)));
+    }
+    // positional segment update
+    if (!placed) {
+      if (p < b + ls) {
+        sz = ls;
+        lnode = 2 * lnode + 1;
+      } else if (p == b + ls) {
+        placed = true;
+      } else {
+        b = b + ls + 1;
+        sz = sz - ls - 1;
+        lnode = 2 * lnode + 2;
+      }
+    }
+  }
+}
+
 // SORT (the selection build): the subtree's elements arrive unsorted in E; the
 // three lists are made in LDS by sorting (orderable coordinate, index) keys,
 // the presort's order. Otherwise they are loaded from the presorted lists.
@@ -743,7 +828,9 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         k[d] = tid < S ? (uint64_t)orderable_key(coord_of(me, d)) << 32 | (uint32_t)__float_as_int(me.w) : ~0ull;
         v[d] = tid;
       }
+#ifndef PM_KD_DIAG_NOSORT
       block_bitonic3(k, v, n2, kx, vx);
+#endif
       __syncthreads();   // buf[2] written; every exchange read
       // (loads only under tid < S: a select between an LDS element and a
       // register value compiled to a flat load through scratch)
@@ -859,90 +946,290 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     if (j >= 0) tag[tid] = (int16_t)(tid < b + ls ? 2 * j : (tid == b + ls ? -1 : 2 * j + 1));
   }
   __syncthreads();
+#ifdef PM_KD_DIAG_NOWAVE
+  if (false) {
+#else
   if (KB < H) {
-  // ---- wave phase: sub-segment j of local level KB (<= 63 elements) -> wave j
-  const int lane = tid & 63, j = tid >> 6;
-  const int cur = KB & 1;
-  const int b0 = sb[cur][j], sz0 = ss[cur][j];
-  const bool active = lane < sz0;
-  float4 e[3];
+#endif
+    // ---- wave phase: sub-segment j of local level KB (<= 63 elements) -> wave j
+    const int lane = tid & 63, j = tid >> 6;
+    const int cur = KB & 1;
+    const int b0 = sb[cur][j], sz0 = ss[cur][j];
+    float4 e[3];
 #pragma unroll
-  for (int d = 0; d < 3; d++) e[d] = active ? buf[d][b0 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-  const int p = b0 + lane;                       // this lane's position (fixed)
-  int b = b0, sz = sz0;                          // this lane's segment
-  int lnode = (1 << KB) - 1 + j;                // local heap index of this lane's segment
-  bool placed = !active;
-  for (int k = KB; k < H && sz0 > 0; k++) {
-    const int ls = placed ? 0 : left_size(sz);
-    // segment extents and median from the lanes holding them (all lanes shuffle)
-    const int lf = placed ? lane : b - b0, ll = placed ? lane : b + sz - 1 - b0;
-    float ext[3];
-#pragma unroll
-    for (int d = 0; d < 3; d++) {
-      const float c = coord_of(e[d], d);
-      ext[d] = __shfl(c, ll) - __shfl(c, lf);
-    }
-    int dim = 0;
-    if (ext[1] > ext[dim]) dim = 1;
-    if (ext[2] > ext[dim]) dim = 2;
-    // per component: a select of whole float4s indexed e[] dynamically,
-    // which kept e[] in scratch for the whole wave phase
-    const bool d0 = dim == 0, d1 = dim == 1;
-    const float4 sel = make_float4(d0 ? e[0].x : (d1 ? e[1].x : e[2].x), d0 ? e[0].y : (d1 ? e[1].y : e[2].y),
-                                   d0 ? e[0].z : (d1 ? e[1].z : e[2].z), d0 ? e[0].w : (d1 ? e[1].w : e[2].w));
-    const int lm = placed ? lane : b + ls - b0;
-    const float4 m = make_float4(__shfl(sel.x, lm), __shfl(sel.y, lm), __shfl(sel.z, lm), __shfl(sel.w, lm));
-    const int nid = __float_as_int(m.w);
-    const float nc = coord_of(m, dim);
-    if (!placed && p == b + ls) stage[lnode] = make_float4(m.x, m.y, m.z, __int_as_float((nid << 2) | dim));
-    if (k + 1 == H) break;
-    // class per list, packed (L, R) counts: list d at bits 14d (L) and 14d + 7 (R)
-    uint8_t c[3];
-    uint64_t cnt = 0;
-#pragma unroll
-    for (int d = 0; d < 3; d++) {
-      c[d] = placed ? 3 : (uint8_t)kd_class(e[d], dim, nc, nid);
-      cnt |= (uint64_t)(c[d] == 0) << (14 * d) | (uint64_t)(c[d] == 2) << (14 * d + 7);
-    }
-    uint64_t inc = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t up = __shfl_up(inc, o);
-      if (lane >= o) inc += up;
-    }
-    const int lb = b - b0 - 1;   // lane before the segment (-1: none)
-    const uint64_t before = __shfl(inc, lb < 0 ? 0 : lb);
-    const uint64_t ex = inc - cnt - (lb < 0 || placed ? 0ull : before);
-    // forward permute of the three elements to their positions in the segment
-#pragma unroll
-    for (int d = 0; d < 3; d++) {
-      int dst = p;
-      if (c[d] == 0) dst = b + (int)((ex >> (14 * d)) & 127);
-      else if (c[d] == 1) dst = b + ls;
-      else if (c[d] == 2) dst = b + ls + 1 + (int)((ex >> (14 * d + 7)) & 127);
-      const int a = (dst - b0) * 4;
-      e[d].x = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].x)));
-      e[d].y = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].y)));
-      e[d].z = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].z)));
-      e[d].w = __int_as_float(__builtin_amdgcn_ds_permute(a, __float_as_int(e[d].w)));
-    }
-    // positional segment update
-    if (!placed) {
-      if (p < b + ls) {
-        sz = ls;
-        lnode = 2 * lnode + 1;
-      } else if (p == b + ls) {
-        placed = true;
-      } else {
-        b = b + ls + 1;
-        sz = sz - ls - 1;
-        lnode = 2 * lnode + 2;
-      }
-    }
-  }
+    for (int d = 0; d < 3; d++) e[d] = lane < sz0 ? buf[d][b0 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    local_wave_levels(e[0], e[1], e[2], lane, j, KB, H, b0, sz0, stage);
   }
   // ---- write-out: nodes leave LDS once, level by level (contiguous heap ranges);
   // a global store inside the level loop made every block barrier wait for it
+  __syncthreads();
+  const float4 nd = stage[tid];
+  if (__float_as_int(nd.w) >= 0) {
+    const int k = 31 - __clz(tid + 1);
+    nodes[(t + 1) * ((int64_t)1 << k) - 1 + (tid + 1 - (1 << k))] = nd;
+  }
+}
+
+// Local finish of the selection build without sorting the three lists
+// (PM_KD_LOCAL_SEL): the block levels (local levels 0 ..
+// KB - 1, <= 8 sub-segments) SELECT each sub-segment's median like the global
+// levels do, on ONE unsorted list in LDS:
+//   extents   the orderable-key min / max of every sub-segment's elements
+//             (wave reductions, one LDS atomic per wave and sub-segment);
+//   histogram 1024 bins per level shared by the sub-segments, the coordinate
+//             key scaled to the sub-segment's key range (monotone: equal keys
+//             share a bin, bins follow the order); the bin holding rank
+//             left_size(sz) is found by one wave per sub-segment;
+//   rank      that bin's elements are appended to a candidate list as unique
+//             (key, index) keys, and each ranks itself among them;
+//   partition every element moves to its child range (unstable: one LDS
+//             atomic per wave, sub-segment and side; the order inside a range
+//             does not matter, the median is defined by rank).
+// The wave levels then sort each <= 63-element sub-segment's three lists in its
+// wave (a 64-lane bitonic network, no barriers) and run local_wave_levels as
+// the sorting finish does. Same rules, same medians, same tree; the sort of
+// 1,024 keys x 3 lists it replaces was 3.0 of k_kd_local<true>'s 6.6 ms per
+// config-3 frame (profiles/r06/r06b_kd_local_nosort_diag.txt).
+#ifndef PM_KD_LOCAL_SEL
+#define PM_KD_LOCAL_SEL 1
+#endif
+constexpr int kLocalBins = 1024;   // histogram bins per block level (all sub-segments)
+
+__device__ __forceinline__ uint32_t key_of(const float4 e, int d) { return orderable_key(coord_of(e, d)); }
+__device__ __forceinline__ float unkey(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// In-wave bitonic sort (ascending) of one (key, slot) pair per lane, 64 lanes.
+__device__ __forceinline__ void wave_bitonic(uint64_t& k, int& v, int lane) {
+#pragma unroll
+  for (int ls = 1; ls <= 6; ls++) {
+    const int size = 1 << ls;
+#pragma unroll
+    for (int lst = ls - 1; lst >= 0; lst--) {
+      const int stride = 1 << lst;
+      const uint64_t pk = (uint64_t)(uint32_t)xor_lane((int)(uint32_t)k, stride) |
+                          (uint64_t)(uint32_t)xor_lane((int)(uint32_t)(k >> 32), stride) << 32;
+      const int pv = xor_lane(v, stride);
+      const bool up = (lane & size) == 0, lower = (lane & stride) == 0;
+      if (lower == up ? pk < k : pk > k) {
+        k = pk;
+        v = pv;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_kd_local_sel(
+    KdSoa E, int L0, SegTab T, float4* __restrict__ nodes) {
+  constexpr int NS = 1 << kLocalWaveLevel;   // sub-segments at the wave level
+  constexpr int NB = NS / 2;                  // <= sub-segments at a block level
+  __shared__ float4 buf[kLocal];              // the elements by position
+  __shared__ float4 stage[kLocal];            // this subtree's nodes by local heap index (w = -1: none)
+  __shared__ uint32_t hist[kLocalBins];
+  __shared__ uint64_t cand[kLocal];           // a sub-segment's candidates at its own positions
+  __shared__ uint32_t kmin[2][NB][3], kmax[2][NB][3];   // per level parity
+  __shared__ int16_t sb[2][NS], ss[2][NS];
+  __shared__ int16_t sls[NB];
+  __shared__ uint32_t sbin[NB], srank[NB], scnt[NB], sl[NB], sr[NB];
+  __shared__ float sco[NB];
+  __shared__ int32_t sid[NB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t t = ((int64_t)1 << L0) - 1 + blockIdx.x;
+  const int B = T.b[t], S = T.s[t];
+  if (S <= 0) return;
+  const int k0 = L0 & 1;
+  float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (tid < S) e = make_float4(E.comp(k0, 0)[B + tid], E.comp(k0, 1)[B + tid], E.comp(k0, 2)[B + tid], E.comp(k0, 3)[B + tid]);
+  int j = tid < S ? 0 : -1;   // sub-segment of this position (-1: placed or empty)
+  stage[tid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+  hist[tid] = 0;
+  if (tid < 2 * NB * 3) {
+    (&kmin[0][0][0])[tid] = 0xFFFFFFFFu;
+    (&kmax[0][0][0])[tid] = 0u;
+  }
+  if (tid == 0) {
+    sb[0][0] = 0;
+    ss[0][0] = (int16_t)S;
+  }
+  const int H = 32 - __clz(S);                 // levels of this subtree
+  const int KB = min(H, kLocalWaveLevel);      // block levels; the rest run per wave
+  __syncthreads();
+  // extents of this position's sub-segment at level k (parity par): per wave,
+  // one reduction and one LDS atomic per sub-segment present
+  auto extents = [&](int par) {
+    uint64_t todo = __builtin_amdgcn_ballot_w64(j >= 0);
+    while (todo) {
+      const int l = __ffsll((long long)todo) - 1;
+      const int sj = __builtin_amdgcn_readlane(j, l);
+      const bool m = j == sj;
+      todo &= ~__builtin_amdgcn_ballot_w64(m);
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        const uint32_t kd = key_of(e, d);
+        const uint32_t mn = wave_minmax<false>(m ? kd : 0xFFFFFFFFu), mx = wave_minmax<true>(m ? kd : 0u);
+        if (lane == l) {
+          atomicMin(&kmin[par][sj][d], mn);
+          atomicMax(&kmax[par][sj][d], mx);
+        }
+      }
+    }
+  };
+  extents(0);
+  for (int k = 0; k < KB; k++) {
+    const int cur = k & 1, nsub = 1 << k, nbin = kLocalBins >> k;
+    __syncthreads();   // extents complete
+    // split dimension, key range and bin of this position's element
+    int dim = 0;
+    uint32_t key = 0, bin = 0;
+    if (j >= 0) {
+      float ext[3];
+#pragma unroll
+      for (int d = 0; d < 3; d++) ext[d] = unkey(kmax[cur][j][d]) - unkey(kmin[cur][j][d]);
+      if (ext[1] > ext[dim]) dim = 1;
+      if (ext[2] > ext[dim]) dim = 2;
+      const uint32_t lo = kmin[cur][j][dim], hi = kmax[cur][j][dim];
+      key = key_of(e, dim);
+      const float scale = (float)nbin / ((float)(hi - lo) + 1.f);
+      bin = min((uint32_t)nbin - 1u, (uint32_t)((float)(key - lo) * scale));
+      atomicAdd(&hist[j * nbin + bin], 1u);
+    }
+    __syncthreads();   // histogram complete
+    // wave w < nsub: sub-segment w's bin holding rank ls; its children's ranges
+    if (wave < nsub) {
+      const int sz = ss[cur][wave], b = sb[cur][wave];
+      const int ls = sz > 0 ? left_size(sz) : 0;
+      if (sz > 0) {
+        constexpr int PER = kLocalBins / 64;   // bins per lane at level 0
+        const int per = PER >> k;              // nbin / 64 (>= 2 at the block levels)
+        uint32_t c[PER];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+          c[q] = q < per ? hist[wave * nbin + lane * per + q] : 0u;
+          sum += c[q];
+        }
+        uint32_t inc = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t up = __shfl_up(inc, o);
+          if (lane >= o) inc += up;
+        }
+        const uint32_t exl = inc - sum;
+        // the lane whose bins cover rank ls
+        if (exl <= (uint32_t)ls && (uint32_t)ls < inc) {
+          uint32_t acc = exl, fb = 0, rr = 0;
+          bool found = false;
+#pragma unroll
+          for (int q = 0; q < PER; q++) {
+            if (!found && q < per && (uint32_t)ls < acc + c[q]) {
+              fb = (uint32_t)(lane * per + q);
+              rr = (uint32_t)ls - acc;
+              found = true;
+            }
+            acc += c[q];
+          }
+          sbin[wave] = fb;
+          srank[wave] = rr;
+        }
+      }
+      if (lane == 0) {
+        sls[wave] = (int16_t)ls;
+        scnt[wave] = 0;
+        sl[wave] = 0;
+        sr[wave] = 0;
+        if (k + 1 < H) {
+          const int nxt = cur ^ 1;
+          sb[nxt][2 * wave] = (int16_t)b;
+          ss[nxt][2 * wave] = (int16_t)(sz > 0 ? ls : 0);
+          sb[nxt][2 * wave + 1] = (int16_t)(b + ls + 1);
+          ss[nxt][2 * wave + 1] = (int16_t)(sz > 0 ? sz - ls - 1 : 0);
+        }
+      }
+    }
+    __syncthreads();   // bins found
+    // the found bin's elements: unique (key, index) candidates
+    const int idx = __float_as_int(e.w);
+    const uint64_t ck = (uint64_t)key << 32 | (uint32_t)idx;
+    const bool isc = j >= 0 && bin == sbin[j];
+    const int cb = j >= 0 ? sb[cur][j] : 0;
+    if (isc) cand[cb + atomicAdd(&scnt[j], 1u)] = ck;
+    hist[tid] = 0;   // this level's histogram is read; the next level's starts at zero
+    if (tid < NB * 3) {   // the next level's extents start empty
+      (&kmin[cur ^ 1][0][0])[tid] = 0xFFFFFFFFu;
+      (&kmax[cur ^ 1][0][0])[tid] = 0u;
+    }
+    __syncthreads();   // candidates complete
+    if (isc) {
+      const uint32_t m = scnt[j];
+      uint32_t r = 0;
+      for (uint32_t i = 0; i < m; i++) r += cand[cb + i] < ck ? 1u : 0u;
+      if (r == srank[j]) {
+        sco[j] = coord_of(e, dim);
+        sid[j] = idx;
+        stage[(1 << k) - 1 + j] = make_float4(e.x, e.y, e.z, __int_as_float((idx << 2) | dim));
+      }
+    }
+    if (k + 1 == H) break;
+    __syncthreads();   // medians known
+    // partition (unstable): left -> [b, b + ls), median -> b + ls, right -> [b + ls + 1, b + sz)
+    int dst = tid;
+    int cls = 3;
+    if (j >= 0) cls = kd_class(e, dim, sco[j], sid[j]);
+    {
+      uint64_t todo = __builtin_amdgcn_ballot_w64(j >= 0);
+      while (todo) {
+        const int l = __ffsll((long long)todo) - 1;
+        const int sj = __builtin_amdgcn_readlane(j, l);
+        const bool m = j == sj;
+        todo &= ~__builtin_amdgcn_ballot_w64(m);
+        const uint64_t ml = __builtin_amdgcn_ballot_w64(m && cls == 0), mr = __builtin_amdgcn_ballot_w64(m && cls == 2);
+        uint32_t bl = 0, br = 0;
+        if (lane == l) {
+          if (ml) bl = atomicAdd(&sl[sj], (uint32_t)__popcll(ml));
+          if (mr) br = atomicAdd(&sr[sj], (uint32_t)__popcll(mr));
+        }
+        bl = (uint32_t)__builtin_amdgcn_readlane((int)bl, l);
+        br = (uint32_t)__builtin_amdgcn_readlane((int)br, l);
+        if (m) {
+          const int b = sb[cur][sj], ls = sls[sj];
+          const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+          if (cls == 0) dst = b + (int)bl + __popcll(ml & lt);
+          else if (cls == 1) dst = b + ls;
+          else dst = b + ls + 1 + (int)br + __popcll(mr & lt);
+        }
+      }
+    }
+    // the position's sub-segment after the move (positions keep their meaning)
+    int nj = -1;
+    if (j >= 0) {
+      const int b = sb[cur][j], ls = sls[j];
+      nj = tid < b + ls ? 2 * j : (tid == b + ls ? -1 : 2 * j + 1);
+    }
+    // (buf was last read at the previous level's reload, several barriers ago)
+    if (tid < S) buf[dst] = e;
+    __syncthreads();
+    if (tid < S) e = buf[tid];
+    j = nj;
+    extents(cur ^ 1);
+  }
+  if (KB < H) {
+    __syncthreads();
+    // ---- wave levels: sub-segment `wave` of local level KB, sorted in the wave
+    const int cur = KB & 1;
+    const int b0 = sb[cur][wave], sz0 = ss[cur][wave];
+    const float4 el = lane < sz0 ? buf[b0 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 es[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      uint64_t kk = lane < sz0 ? (uint64_t)key_of(el, d) << 32 | (uint32_t)__float_as_int(el.w) : ~0ull;
+      int v = lane;
+      wave_bitonic(kk, v, lane);
+      es[d] = make_float4(__shfl(el.x, v), __shfl(el.y, v), __shfl(el.z, v), __shfl(el.w, v));
+    }
+    local_wave_levels(es[0], es[1], es[2], lane, wave, KB, H, b0, sz0, stage);
+  }
+  // ---- write-out: nodes leave LDS once, level by level (contiguous heap ranges)
   __syncthreads();
   const float4 nd = stage[tid];
   if (__float_as_int(nd.w) >= 0) {
@@ -1973,7 +2260,8 @@ static hipError_t kd_build_sel(const float4* elems, int64_t n, float4* nodes, hi
     k_ks_part<<<(int)ntiles, kSelThreads, 0, s>>>(E, n, T, S, L, tile_seg.p);
     PM_HIP_TRY(hipGetLastError());
   }
-  k_kd_local<true><<<(int)nsc, kLocal, 0, s>>>(KdLists{}, E, L0, T, nodes);
+  if (PM_KD_LOCAL_SEL) k_kd_local_sel<<<(int)nsc, kLocal, 0, s>>>(E, L0, T, nodes);
+  else k_kd_local<true><<<(int)nsc, kLocal, 0, s>>>(KdLists{}, E, L0, T, nodes);
   return hipGetLastError();
 }
 
