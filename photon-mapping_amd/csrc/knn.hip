@@ -702,54 +702,11 @@ __device__ __forceinline__ float subtree_cut(const float4* __restrict__ nodes, u
 // from the leaders. TAG only separates the global-map launches into their own
 // kernel symbol (rocprof). perm: lane of walk rank r takes query perm[r] and
 // writes its result there (Morton walk order without permuted copies).
-// XCD-aware dynamic assignment (PM_GATHER_XCD): the items [0, t1) are split
-// into 8 contiguous ranges of the walk order, one per XCD, and each wave takes
-// the next 64 items of its own XCD's range (HW_REG_XCC_ID) when it starts, or,
-// once that range is empty, of the next XCDs' ranges. So each XCD's L2 serves
-// a compact region of the walk order while the load stays balanced: round 4's
-// fixed XCD-contiguous block order halved the L2 misses but left the XCDs with
-// the long walks busy while the others idled (51 vs 41 ms). Placement changes
-// only speed; every item is taken exactly once (the launch has at least as
-// many waves as there are chunks). xctr[x]: items of range x taken.
-#ifndef PM_GATHER_XCD
-#define PM_GATHER_XCD 0   // measured slower: profiles/r06/r06d_gather_xcd_ab.log (49.8 vs 41.0 ms)
-#endif
-__device__ __forceinline__ uint32_t xcc_id() {
-  uint32_t x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-  return x & 7u;
-}
-// first item of this wave's chunk (-1: none left) and the end of its range
-__device__ __forceinline__ int64_t xcd_chunk(unsigned long long* __restrict__ xctr, int64_t t1, int64_t& hi) {
-  const uint32_t home = xcc_id();
-  for (uint32_t q = 0; q < 8; q++) {
-    const int x = (int)((home + q) & 7u);
-    const int64_t lo = t1 * x / 8, h = t1 * (x + 1) / 8;
-    unsigned long long g = 0;
-    if ((threadIdx.x & 63) == 0) g = atomicAdd(xctr + x, 64ull);
-    g = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
-        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
-    if (lo + (int64_t)g < h) {
-      hi = h;
-      return lo + (int64_t)g;
-    }
-  }
-  hi = 0;
-  return -1;
-}
-
-// One level of the seeded gather. LEADERS: walk ranks 0, S, 2S, ... with the
-// plain cut-off, recording (position, K-th d^2) in lead[Seeds::index(r)]; followers:
-// every other rank (thread t -> rank (t / (S-1)) * S + 1 + t % (S-1)), cut-off
-// from the leaders. TAG only separates the global-map launches into their own
-// kernel symbol (rocprof). perm: lane of walk rank r takes query perm[r] and
-// writes its result there (Morton walk order without permuted copies).
 template <int TAG, bool LEADERS, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && (kGatherBox == 1 || kGatherBox == 2) ? 3 : 4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
-    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx, int64_t t1,
-    unsigned long long* __restrict__ xctr) {
+    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx, int64_t t1) {
   // lanes [0, t1): leader index (rank t S) or follower index
   __shared__ double lq[(kGatherQL + 1) * 256];
   const float R2 = kKMaxDistance * kKMaxDistance;
@@ -765,13 +722,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
     const uint32_t e = bid * 256u + threadIdx.x;
     valid = e < *nretry;
     r = valid ? (int64_t)retry[e] : 0;
-  } else if (xctr) {   // XCD-aware dynamic assignment (xcd_chunk)
-    int64_t hi;
-    const int64_t t0 = xcd_chunk(xctr, t1, hi);
-    const int64_t t = t0 + (threadIdx.x & 63);
-    r = LEADERS ? Seeds<kSeedGroup>::leader_rank(t) : Seeds<kSeedGroup>::follower_rank(t);
-    valid = t0 >= 0 && t < hi && r < nq;
-    if (t0 < 0) return;   // wave-uniform: every range is taken
   } else {
     const int64_t t = ((int64_t)bid - nrb) * blockDim.x + threadIdx.x;
     r = LEADERS ? Seeds<kSeedGroup>::leader_rank(t) : Seeds<kSeedGroup>::follower_rank(t);
@@ -978,30 +928,19 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   const bool wide = PM_FORCE_WIDE || n >= (1 << 28);
   uint32_t* const rt = kLeaderBudget > 0 ? retry.p : nullptr;
   uint32_t* const nrt = kLeaderBudget > 0 ? nretry.p : nullptr;
-  // XCD-aware dynamic assignment: range counters per launch (leaders, followers)
-  DevBuf<unsigned long long> xctr(PM_GATHER_XCD ? 16 : 0);
-  if (PM_GATHER_XCD) {
-    if (!xctr.p) return hipErrorOutOfMemory;
-    PM_HIP_TRY(hipMemsetAsync(xctr.p, 0, 16 * sizeof(unsigned long long), s));
-  }
   // one launch of k_gather_level<tag, LEADERS, wide> over lanes [0, t1)
   auto level = [&](auto leaders, int grid, int rb, int64_t t1) -> hipError_t {
     constexpr bool L = decltype(leaders)::value;
     if (grid <= 0) return hipSuccess;
     const float4 *nd = m->nodes.p, *pl = m->payload.p;
-    unsigned long long* xc = nullptr;
-    if (PM_GATHER_XCD) {   // each range's last chunk may be partial: up to 8 more chunks than waves
-      xc = xctr.p + (L ? 0 : 8);
-      grid += 2;
-    }
     if (tag == 1 && wide)
-      k_gather_level<1, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, xc);
+      k_gather_level<1, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     else if (tag == 1)
-      k_gather_level<1, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, xc);
+      k_gather_level<1, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     else if (wide)
-      k_gather_level<0, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, xc);
+      k_gather_level<0, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     else
-      k_gather_level<0, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, xc);
+      k_gather_level<0, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
     return hipGetLastError();
   };
   // leaders (walk ranks 0, S, 2S, ...), then the followers with the retry
