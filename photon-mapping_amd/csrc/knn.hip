@@ -702,6 +702,28 @@ __device__ __forceinline__ float subtree_cut(const float4* __restrict__ nodes, u
 // from the leaders. TAG only separates the global-map launches into their own
 // kernel symbol (rocprof). perm: lane of walk rank r takes query perm[r] and
 // writes its result there (Morton walk order without permuted copies).
+// Windowed XCD swizzle of the walk order (PM_GATHER_XCD_K = k > 0): blocks are
+// dealt round-robin over the 8 XCDs, so block b's XCD label is b % 8; inside
+// every window of 8k consecutive blocks the k blocks that share a label take
+// k consecutive 256-rank pieces of the window's walk range. The GPU still
+// works on one coherent frontier of the walk order (round 6: giving each XCD
+// a whole eighth of the order instead was 49.8 vs 41.0 ms), but each XCD's L2
+// serves a compact eighth of it. f: the block's index among the launch's
+// walk blocks, bid: its grid index (the label). The tail window keeps f.
+// Config 3's global gather (ms, alternating runs, profiles/r06/r06e_*):
+// k = 0 (the plain order) 41.1-41.4, 4 40.7-40.9, 8 40.2-40.5, 16 39.9-40.3,
+// 32 39.9-40.2, 128 40.2-40.4; config 2's 4.27-4.38 / 4.27 / 4.17-4.26 /
+// 4.24-4.34 / 4.15-4.25 / 4.51: 32.
+#ifndef PM_GATHER_XCD_K
+#define PM_GATHER_XCD_K 32
+#endif
+__device__ __forceinline__ uint32_t xcd_window_block(uint32_t f, uint32_t bid) {
+  constexpr uint32_t K = PM_GATHER_XCD_K, W = 8 * K;
+  if (K == 0 || f >= gridDim.x - (bid - f) - (gridDim.x - (bid - f)) % W) return f;   // tail window: as is
+  const uint32_t w0 = f - f % W;
+  return w0 + (bid % 8u) * K + (f % W) / 8u;
+}
+
 template <int TAG, bool LEADERS, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && (kGatherBox == 1 || kGatherBox == 2) ? 3 : 4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
@@ -723,7 +745,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
     valid = e < *nretry;
     r = valid ? (int64_t)retry[e] : 0;
   } else {
-    const int64_t t = ((int64_t)bid - nrb) * blockDim.x + threadIdx.x;
+    const int64_t t = (int64_t)xcd_window_block(bid - (uint32_t)nrb, bid) * blockDim.x + threadIdx.x;
     r = LEADERS ? Seeds<kSeedGroup>::leader_rank(t) : Seeds<kSeedGroup>::follower_rank(t);
     valid = t < t1 && r < nq;
   }
