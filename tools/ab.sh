@@ -14,6 +14,30 @@ if [ -n "${TESTS:-}" ]; then
     > gpurun_out/ab/tests.log 2>&1 || { tail -40 gpurun_out/ab/tests.log; exit 1; }
   tail -1 gpurun_out/ab/tests.log
 fi
+# STATS="regex": instead of the bench lines, each entry's rocprofv3 --kernel-trace
+# --stats of `bench.py $ARGS --steps 2 --warmup 1`: ms per frame of the kernels
+# whose names match
+if [ -n "${STATS:-}" ]; then
+  export TMPDIR=/tmp
+  R=$(pwd)
+  for e in "$@"; do
+    v=${e%%@*}
+    X=""
+    [ "$e" != "$v" ] && X=$(echo "${e#*@}" | tr ',' ' ')
+    tag=$(echo "$e" | tr -c 'a-zA-Z0-9_\n' '_')
+    (cd /tmp && PM_HIP_LIB=$R/photon-mapping_amd/$v/libpm_hip.so timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d $R/gpurun_out/ab/st_$tag -o s -- python3 $R/bench.py ${ARGS:-} $X --steps 2 --warmup 1 \
+      --no-cpu-baseline --no-secondary > $R/gpurun_out/ab/st_$tag.log 2>&1) || { echo "STATS_FAILED $e"; exit 4; }
+    python3 - "$e" "$(ls gpurun_out/ab/st_$tag/*/s_kernel_stats.csv gpurun_out/ab/st_$tag/s_kernel_stats.csv 2>/dev/null | head -1)" "$STATS" <<'PY'
+import csv, re, sys
+e, f, pat = sys.argv[1:4]
+for r in csv.DictReader(open(f)):
+    if re.search(pat, r["Name"]):
+        print(f"{e:28s} {r['Name'][:60]:60s} calls {r['Calls']:>4s} ms/frame {float(r['TotalDurationNs']) / 3e6:8.3f}", flush=True)
+PY
+  done
+  exit 0
+fi
 for rep in $(seq ${REPS:-2}); do
   for e in "$@"; do
     v=${e%%@*}
