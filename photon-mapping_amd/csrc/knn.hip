@@ -1197,35 +1197,6 @@ constexpr int kWideLeaderBudget = PM_WIDE_LEADER_BUDGET;
 #ifndef PM_WIDE_WAVES
 #define PM_WIDE_WAVES 0
 #endif
-// The persistent wide gather's work order, windowed over the XCDs as
-// k_gather_level's blocks are (xcd_window_block): XCD x takes the groups
-// (8 w + x) K + j (window w, j < K) in that order from its own counter
-// (HW_REG_XCC_ID), so each XCD's L2 serves a compact slice of the one walk
-// frontier; once its slices are used up a wave takes another XCD's, so every
-// group is taken exactly once. counter[0 .. 8): the XCDs' sequences.
-#ifndef PM_WIDE_XCD_K
-#define PM_WIDE_XCD_K 0   // 128 measured as noise: profiles/r06/r06h_pool_and_wide_xcd_ab.log
-#endif
-__device__ __forceinline__ uint32_t xcc_id() {
-  uint32_t x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-  return x & 7u;
-}
-__device__ __forceinline__ int64_t wide_group(uint32_t* __restrict__ counter, int64_t ngroups, uint32_t home,
-                                              uint32_t& steal) {
-  constexpr int64_t K = PM_WIDE_XCD_K;
-  while (steal < 8) {
-    const uint32_t x = K > 0 ? (home + steal) & 7u : 0u;
-    uint32_t i = 0;
-    if ((threadIdx.x & 63) == 0) i = atomicAdd(counter + x, 1u);
-    i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
-    const int64_t g = K > 0 ? ((int64_t)(i / K) * 8 + x) * K + i % K : (int64_t)i;
-    if (g < ngroups) return g;
-    steal = K > 0 ? steal + 1 : 8;   // x's sequence is increasing: it is used up
-  }
-  return -1;
-}
-
 template <int TAG, bool LEADERS, bool WIDE, int S>
 __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wide(const float4* __restrict__ nodes,
                                                      const float4* __restrict__ payload, int n,
@@ -1253,13 +1224,12 @@ __global__ __launch_bounds__(256) PM_WAVES_ATTR(PM_WIDE_WAVES) void k_gather_wid
   // count is the leader launch's, complete before this launch starts)
   const int64_t nre = (!LEADERS && kWideLeaderBudget > 0) ? (int64_t)*nretry : 0;
   const int64_t items = nitems + nre;
-  const int64_t ngroups = (items + 63) / 64;
-  const uint32_t home = xcc_id();
-  uint32_t steal = 0;   // wave-uniform: XCD sequences found used up
   for (;;) {
-    const int64_t g = wide_group(counter, ngroups, home, steal);
-    if (g < 0) break;   // wave-uniform: every wave reaches it
-    const int64_t t0 = g * 64 + lane;
+    uint32_t g = 0;
+    if (lane == 0) g = atomicAdd(counter, 1u);
+    g = __shfl(g, 0);
+    if ((int64_t)g * 64 >= items) break;   // wave-uniform: every wave reaches it
+    const int64_t t0 = (int64_t)g * 64 + lane;
     const bool redo = t0 < nre;             // a retried leader
     const int64_t t = t0 - nre;
     int64_t r;
@@ -1416,12 +1386,11 @@ static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb,
     per_cu = 4;
   const int64_t wg = std::min<int64_t>((groups + 3) / 4, (int64_t)device_cus() * per_cu);
   DevBuf<float4> lead(nl);
-  // ctr[0 .. 8) / [8 .. 16): the leader / follower launch's XCD sequences, ctr[16]: retried leaders
-  DevBuf<uint32_t> ctr(17), retry(kWideLeaderBudget > 0 ? nl : 1);
+  DevBuf<uint32_t> ctr(3), retry(kWideLeaderBudget > 0 ? nl : 1);   // ctr[2]: retried leaders
   DevBuf<double> rows((size_t)wg * 256 * CAP);
   DevBuf<float4> box(2 * (size_t)std::max<int64_t>(boxed_nodes(n, PM_WIDE_BOX_SKIP), 1));
   if (!lead.p || !ctr.p || !rows.p || !box.p || !retry.p) return hipErrorOutOfMemory;
-  PM_HIP_TRY(hipMemsetAsync(ctr.p, 0, 17 * sizeof(uint32_t), s));
+  PM_HIP_TRY(hipMemsetAsync(ctr.p, 0, 3 * sizeof(uint32_t), s));
   int64_t nbox = 0;
   PM_HIP_TRY(build_subtree_boxes(m->nodes.p, n, PM_WIDE_BOX_SKIP, box.p, &nbox, s));
   BoxView bx;
@@ -1430,12 +1399,12 @@ static hipError_t launch_gather_wide_s(const pm_photon_map* m, const float4* qb,
   const bool wide = PM_FORCE_WIDE || n >= (1 << 28);
 #define PM_WIDE_LAUNCH(W)                                                                                          \
   k_gather_wide<0, true, W, S><<<(int)std::min<int64_t>(wg, (nl + 255) / 256), 256, 0, s>>>(                     \
-      m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p, nl, bx, retry.p, ctr.p + 16);      \
+      m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p, nl, bx, retry.p, ctr.p + 2);      \
   PM_HIP_TRY(hipGetLastError());                                                                                 \
   if (nf > 0 || kWideLeaderBudget > 0) {                                                                          \
     k_gather_wide<0, false, W, S><<<(int)std::min<int64_t>(wg, (nf + nl + 255) / 256), 256, 0, s>>>(             \
-        m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p + 8, nf, bx, retry.p,           \
-        ctr.p + 16);                                                                                             \
+        m->nodes.p, m->payload.p, n, qb, nq, out, perm, lead.p, k, rows.p, ctr.p + 1, nf, bx, retry.p,           \
+        ctr.p + 2);                                                                                              \
     PM_HIP_TRY(hipGetLastError());                                                                               \
   }
   if (wide) {

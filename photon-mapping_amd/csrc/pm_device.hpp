@@ -545,29 +545,10 @@ inline int64_t pool_grid(int64_t np, int block) {
 #ifndef PM_POOL_REFILL
 #define PM_POOL_REFILL 16
 #endif
-// Windowed XCD swizzle of a grid's work chunks (as the gather's, knn.hip
-// xcd_window_block): blocks are dealt round-robin over the 8 XCDs (block b's
-// label b % 8); inside each window of 8K consecutive blocks, the K blocks that
-// share a label take K consecutive chunks, so each XCD's L2 serves a compact
-// slice of the one frontier. Speed only: a bijection on the blocks.
-#ifndef PM_POOL_XCD_K
-#define PM_POOL_XCD_K 0   // noise: profiles/r06/r06h_pool_and_wide_xcd_ab.log
-#endif
-template <uint32_t K>
-__device__ __forceinline__ uint32_t window_chunk(uint32_t b, uint32_t nb) {
-  if constexpr (K == 0) {
-    (void)nb;
-    return b;
-  } else {
-    constexpr uint32_t W = 8 * K;
-    if (b >= nb - nb % W) return b;   // tail window: as is
-    return (b - b % W) + (b % 8u) * K + (b % W) / 8u;
-  }
-}
 template <bool ANY, typename Fetch, typename Done>
 __device__ __forceinline__ void traverse_pool(const DevScene& S, int* stack, int stride, int* overflow, int64_t n,
                                               int chunk, int* lnext, Fetch fetch, Done done) {
-  const int64_t cbase = (int64_t)window_chunk<PM_POOL_XCD_K>(blockIdx.x, gridDim.x) * chunk;
+  const int64_t cbase = (int64_t)blockIdx.x * chunk;
   const int cn = (int)(n - cbase < chunk ? n - cbase : chunk);
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
