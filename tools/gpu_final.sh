@@ -4,7 +4,7 @@
 # tools/wide_prof_summary.py). PART=a: -m gpu suite, smoke, profiles_run.sh +
 # box-side pmc_summary (so the bench line carries roofline.traffic), frame
 # timeline, the default bench line. PART=b: config 2 and config 5 bench lines,
-# the wide gather's stats + PMC.
+# the wide gather's stats + PMC, the per-rank N = 2 / 4 / 8 projection.
 set -u
 cd ${GRAFT_REPO_ROOT:-.}
 TAG=${1:-r04x}
@@ -26,5 +26,8 @@ else
   timeout -k 10 300 python -u bench.py --config 5 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_c5.log 2>&1 || { echo BENCH_C5_FAILED; tail -20 gpurun_out/bench_c5.log; exit 7; }
   tail -1 gpurun_out/bench_c5.log | cut -c1-300
   LIB=lib bash tools/gpu_wide_prof.sh || exit 8
+  # per-rank cost at N = 2 / 4 / 8 on this one GPU, every rank
+  WORLDS="2 4 8" timeout -k 10 900 python -u tools/rank_projection.py > gpurun_out/rank_projection.jsonl 2> gpurun_out/rank_projection_ranks.log || { echo PROJ_FAILED; tail -20 gpurun_out/rank_projection_ranks.log; exit 9; }
+  cat gpurun_out/rank_projection.jsonl | cut -c1-300
 fi
 echo final-done
