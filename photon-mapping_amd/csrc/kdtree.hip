@@ -994,6 +994,21 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 #define PM_KD_LOCAL_SEL 1
 #endif
 constexpr int kLocalBins = 1024;   // histogram bins per block level (all sub-segments)
+// PM_KD_DIAG_TIME (diagnostic builds only): thread 0 of each local-finish
+// workgroup stamps clock64() at its phase boundaries; pm_diag_kd_stamps copies
+// them out (tools/kd_local_diag.py).
+#ifdef PM_KD_DIAG_TIME
+constexpr int kDiagBlocks = 1 << 16, kDiagStamps = 8;
+__device__ unsigned long long g_kd_stamp[kDiagBlocks * kDiagStamps];
+#define KD_STAMP(i)                                                                            \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < kDiagBlocks) g_kd_stamp[blockIdx.x * kDiagStamps + (i)] = clock64(); \
+  } while (0)
+#else
+#define KD_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 __device__ __forceinline__ uint32_t key_of(const float4 e, int d) { return orderable_key(coord_of(e, d)); }
 __device__ __forceinline__ float unkey(uint32_t k) {
@@ -1039,11 +1054,12 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
   const int B = T.b[t], S = T.s[t];
   if (S <= 0) return;
   const int k0 = L0 & 1;
+  KD_STAMP(0);
   float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
   if (tid < S) e = make_float4(E.comp(k0, 0)[B + tid], E.comp(k0, 1)[B + tid], E.comp(k0, 2)[B + tid], E.comp(k0, 3)[B + tid]);
   int j = tid < S ? 0 : -1;   // sub-segment of this position (-1: placed or empty)
   stage[tid] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-  hist[tid] = 0;
+  for (int i = tid; i < kLocalBins; i += kLocal) hist[i] = 0;
   if (tid < 2 * NB * 3) {
     (&kmin[0][0][0])[tid] = 0xFFFFFFFFu;
     (&kmax[0][0][0])[tid] = 0u;
@@ -1076,6 +1092,7 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     }
   };
   extents(0);
+  KD_STAMP(1);
   for (int k = 0; k < KB; k++) {
     const int cur = k & 1, nsub = 1 << k, nbin = kLocalBins >> k;
     __syncthreads();   // extents complete
@@ -1154,7 +1171,7 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const bool isc = j >= 0 && bin == sbin[j];
     const int cb = j >= 0 ? sb[cur][j] : 0;
     if (isc) cand[cb + atomicAdd(&scnt[j], 1u)] = ck;
-    hist[tid] = 0;   // this level's histogram is read; the next level's starts at zero
+    for (int i = tid; i < kLocalBins; i += kLocal) hist[i] = 0;   // this level's histogram is read; the next starts at zero
     if (tid < NB * 3) {   // the next level's extents start empty
       (&kmin[cur ^ 1][0][0])[tid] = 0xFFFFFFFFu;
       (&kmax[cur ^ 1][0][0])[tid] = 0u;
@@ -1212,6 +1229,7 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     if (tid < S) e = buf[tid];
     j = nj;
     extents(cur ^ 1);
+    if (k < 4) KD_STAMP(2 + k);
   }
   if (KB < H) {
     __syncthreads();
@@ -1227,6 +1245,7 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
       wave_bitonic(kk, v, lane);
       es[d] = make_float4(__shfl(el.x, v), __shfl(el.y, v), __shfl(el.z, v), __shfl(el.w, v));
     }
+    KD_STAMP(6);
     local_wave_levels(es[0], es[1], es[2], lane, wave, KB, H, b0, sz0, stage);
   }
   // ---- write-out: nodes leave LDS once, level by level (contiguous heap ranges)
@@ -1236,6 +1255,7 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const int k = 31 - __clz(tid + 1);
     nodes[(t + 1) * ((int64_t)1 << k) - 1 + (tid + 1 - (1 << k))] = nd;
   }
+  KD_STAMP(7);
 }
 
 // ------------------------------------------------------------------ selection build
@@ -1271,7 +1291,10 @@ __global__ __launch_bounds__(kLocal) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 #ifndef PM_KS_NSUB
 #define PM_KS_NSUB 4   // sub-tiles per block (one subtree prologue for all of them)
 #endif
-constexpr int kSelThreads = 256;
+#ifndef PM_KS_THREADS
+#define PM_KS_THREADS 256   // threads per block of the per-position selection kernels
+#endif
+constexpr int kSelThreads = PM_KS_THREADS;
 constexpr int kSelIPT = PM_KS_IPT;
 constexpr int kSelTile = kSelThreads * kSelIPT;   // positions per sub-tile
 constexpr int kSelNSub = PM_KS_NSUB;
@@ -1935,7 +1958,11 @@ __global__ __launch_bounds__(kCandThreads) void k_ks_cand(int level, SegTab T, S
 // instead of five, reading the split coordinate twice (the second time from L2).
 constexpr int kSegSelMax = 1 << 17;
 #ifndef PM_KS_SEGSEL_MIN
-#define PM_KS_SEGSEL_MIN 512   // subtrees per level for k_ks_segsel (fewer workgroups underfill the GPU)
+// subtrees per level for k_ks_segsel (fewer workgroups underfill the GPU).
+// Round 6, config 3 (profiles/r06/r06j_*): 512 sent level 9 (512 subtrees of
+// ~89 k elements, 2 workgroups per CU) here at 2.2 ms; 1024 gives it to the
+// grid-wide passes: kd phase -0.3 ms; 2048: no further change
+#define PM_KS_SEGSEL_MIN 1024
 #endif
 constexpr int64_t kSegSelMinSegs = PM_KS_SEGSEL_MIN;
 #ifndef PM_KS_SEGSEL_U
@@ -2494,3 +2521,10 @@ hipError_t launch_map_export(const pm_photon_map* m, pm_kd_photon* out, hipStrea
 }
 
 }  // namespace pmd
+
+#ifdef PM_KD_DIAG_TIME
+extern "C" int pm_diag_kd_stamps(unsigned long long* out, long long n) {
+  if (n > (long long)pmd::kDiagBlocks * pmd::kDiagStamps) n = (long long)pmd::kDiagBlocks * pmd::kDiagStamps;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pmd::g_kd_stamp), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -625,11 +625,47 @@ constexpr int kGatherBox = PM_GATHER_BOX;
 #endif
 constexpr int kBoxAfter = PM_BOX_AFTER;
 
-__device__ __forceinline__ double seed_bound(float4 lead, v3 q) {
-  if (!(lead.w >= 0.f)) return 1e300;
+// Guessed follower cut-offs (round 6, PM_SEED_GUESS). The K-th nearest
+// distance r(x) is 1-Lipschitz, so r_f <= r_L + d (d = |f - L|) holds for a
+// follower f and any leader L: seed_bound. It is loose wherever the density
+// varies slowly, which is almost everywhere: a follower walks with the tighter
+// GUESS min(r_L + d, r_L (1 + beta) + alpha d) instead. A follower whose list
+// does not fill under a guess (fewer than K photons inside it) is not written:
+// its walk rank goes to a retry list, and k_gather_fretry re-walks it with the
+// guaranteed cut-off after the follower launch. A list that does fill holds
+// the K nearest (every point inside the cut-off was visited), the same keys
+// the guaranteed walk finds, so every result is bitwise the production one.
+// Config 3 (guess only, misses not re-walked; profiles/r06/r06k_*): alpha /
+// beta 0.5 / 0.1: 0.009 % misses, 0.25 / 0.1: 0.33 % (gather -2.2 ms), 0 / 0.3:
+// 3 % (-3.7 ms), 0 / 0.2: 10 % (-5.2 ms); a retried walk costs about what a
+// leader's does (~3 follower walks: its neighbours in the retry list are far).
+#ifndef PM_SEED_GUESS
+#define PM_SEED_GUESS 1
+#endif
+#ifndef PM_SEED_GUESS_ALPHA
+#define PM_SEED_GUESS_ALPHA 0.25
+#endif
+#ifndef PM_SEED_GUESS_BETA
+#define PM_SEED_GUESS_BETA 0.1
+#endif
+constexpr bool kSeedGuess = PM_SEED_GUESS;
+__device__ __forceinline__ double seed_sq(double c) { return c * c * (1.0 + 1e-5) + 1e-30; }
+// (guaranteed, guessed) squared bounds of follower q from one leader record
+__device__ __forceinline__ void seed_bounds(float4 lead, v3 q, double& guar, double& guess) {
+  if (!(lead.w >= 0.f)) {
+    guar = guess = 1e300;
+    return;
+  }
   const double dx = (double)q.x - lead.x, dy = (double)q.y - lead.y, dz = (double)q.z - lead.z;
-  const double c = (sqrt((double)lead.w) + sqrt(dx * dx + dy * dy + dz * dz)) * (1.0 + 1e-6);
-  return c * c * (1.0 + 1e-5) + 1e-30;
+  const double rl = sqrt((double)lead.w), dl = sqrt(dx * dx + dy * dy + dz * dz);
+  const double c = rl + dl;
+  guar = seed_sq(c * (1.0 + 1e-6));
+  guess = seed_sq(fmin(c, rl * (1.0 + PM_SEED_GUESS_BETA) + PM_SEED_GUESS_ALPHA * dl) * (1.0 + 1e-6));
+}
+__device__ __forceinline__ double seed_bound(float4 lead, v3 q) {
+  double g, e;
+  seed_bounds(lead, q, g, e);
+  return g;
 }
 // f32 cut-off >= bound (rounded up), capped at the plain cut-off
 __device__ __forceinline__ float seed_cut(double bound, float r2) {
@@ -640,17 +676,26 @@ __device__ __forceinline__ float seed_cut(double bound, float r2) {
   return fminf(f, plain);
 }
 
-// cut-off of walk rank r (a follower) from the leaders' records
+// cut-off of walk rank r (a follower) from the leaders' records: the
+// guaranteed one, and in *guess (kSeedGuess) the guessed one (<= guaranteed)
 template <int G>
 __device__ __forceinline__ float follower_cut(const float4* __restrict__ lead, int64_t nq, int64_t r, v3 q,
-                                              float R2) {
+                                              float R2, float* guess = nullptr) {
   const int64_t jp = Seeds<G>::before(r), ns = Seeds<G>::count(nq);
-  double b = seed_bound(lead[jp], q);
-  if (jp + 1 < ns) b = fmin(b, seed_bound(lead[jp + 1], q));
+  double b, e;
+  seed_bounds(lead[jp], q, b, e);
+  auto more = [&](int64_t j) {
+    double b1, e1;
+    seed_bounds(lead[j], q, b1, e1);
+    b = fmin(b, b1);
+    e = fmin(e, e1);
+  };
+  if (jp + 1 < ns) more(jp + 1);
   if (kSeedLeaders > 2) {
-    if (jp >= 1) b = fmin(b, seed_bound(lead[jp - 1], q));
-    if (jp + 2 < ns) b = fmin(b, seed_bound(lead[jp + 2], q));
+    if (jp >= 1) more(jp - 1);
+    if (jp + 2 < ns) more(jp + 2);
   }
+  if (guess) *guess = seed_cut(e, R2);
   return seed_cut(b, R2);
 }
 
@@ -738,9 +783,16 @@ template <int TAG, bool LEADERS, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && (kGatherBox == 1 || kGatherBox == 2) ? 3 : 4))) void k_gather_level(
     const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
     int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, float4* __restrict__ lead,
-    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx, int64_t t1) {
+    uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry, int retry_blocks, BoxView bx, int64_t t1,
+    uint8_t* __restrict__ missed) {
   // lanes [0, t1): leader index (rank t S) or follower index
-  __shared__ double lq[(kGatherQL + 1) * 256];
+  // + one slot per lane: a follower walking under a guessed cut-off parks its
+  // guaranteed cut-off (low word) and walk rank (high word) there, off the
+  // VGPRs the walk needs (~0: not guessed)
+  __shared__ double lq[(kGatherQL + 2) * 256];
+  uint64_t* const park = reinterpret_cast<uint64_t*>(lq + threadIdx.x + (kGatherQL + 1) * 256);
+  const bool guessing = !LEADERS && kSeedGuess && missed;
+  if (guessing) *park = ~0ull;
   const float R2 = kKMaxDistance * kKMaxDistance;
   // follower launch with a leader budget: the first nretry_blocks workgroups
   // (one lane per leader) re-walk the leaders that ran out of budget, with the
@@ -776,6 +828,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
         const float t = lead[Seeds<kSeedGroup>::index(r)].w;
         if (t >= 0.f) cut = fminf(cut, t);
       }
+    } else if (guessing) {
+      float g;
+      const float gc = follower_cut<kSeedGroup>(lead, nq, r, q, R2, &g);
+      cut = g;
+      if (g < gc) *park = (uint64_t)(uint32_t)r << 32 | __float_as_uint(gc);
     } else {
       cut = follower_cut<kSeedGroup>(lead, nq, r, q, R2);
     }
@@ -797,6 +854,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
     const bool full = gkey_word(list[kKNearest - 1]) != kNoWord;
     const v3 f = radiance_g(list, payload, qq.w, full ? gkey_d2(list[kKNearest - 1]) : R2);
     out[i] = make_float4(f.x, f.y, f.z, 0.f);
+    // a guessed cut-off that held fewer than K photons: flagged by walk rank;
+    // k_gather_fmark lists the flags in walk order, k_gather_fretry re-walks
+    // them with the guaranteed cut-off and overwrites their slots
+    if (guessing && !full) {
+      const uint64_t pk = *park;
+      if (pk != ~0ull) missed[pk >> 32] = 1;
+    }
     if (LEADERS) lead[Seeds<kSeedGroup>::index(r)] = make_float4(qq.x, qq.y, qq.z, full ? gkey_d2(list[kKNearest - 1]) : -1.f);
   }
   if (LEADERS && kLeaderBudget > 0) {
@@ -812,6 +876,103 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEADERS && 
       if (lane == first) base = atomicAdd(nretry, (uint32_t)__popcll(m));
       base = __shfl(base, first);
       if (redo) retry[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint32_t)r;
+    }
+  }
+}
+
+// The follower retry list (kSeedGuess), in walk order: the walk ranks whose
+// miss flag the follower launch set. A block takes 16,384 consecutive flags
+// (64 per thread, four 16-B loads), counts them, reserves its range with ONE
+// atomic and writes its ranks there in order (one atomic per wave cost 0.4 ms:
+// ~10^5 misses on one address). The list fills `retry` downwards from entry
+// nq - 1 (the leaders' budget retries use it upwards from 0: at most
+// nl + nf = nq entries), counted in nretry[1].
+constexpr int kMarkPer = 64;   // flags per thread
+__global__ __launch_bounds__(256) void k_gather_fmark(const uint8_t* __restrict__ missed, int64_t nq,
+                                                      uint32_t* __restrict__ retry, uint32_t* __restrict__ nretry) {
+  __shared__ uint32_t wtot[4];
+  __shared__ uint32_t sbase;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int64_t r0 = (int64_t)blockIdx.x * 256 * kMarkPer; r0 < nq; r0 += (int64_t)gridDim.x * 256 * kMarkPer) {
+    const int64_t rb = r0 + (int64_t)threadIdx.x * kMarkPer;
+    uint4 f[kMarkPer / 16];
+#pragma unroll
+    for (int k = 0; k < kMarkPer / 16; k++) {
+      const int64_t p = rb + 16 * k;
+      if (p + 16 <= nq) {
+        f[k] = *reinterpret_cast<const uint4*>(missed + p);
+      } else {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int j = 0; j < 16; j++)
+          if (p + j < nq) w[j >> 2] |= (uint32_t)missed[p + j] << (8 * (j & 3));
+        f[k] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+    uint32_t c = 0;   // flags are 0 / 1 bytes
+#pragma unroll
+    for (int k = 0; k < kMarkPer / 16; k++) c += __popc(f[k].x) + __popc(f[k].y) + __popc(f[k].z) + __popc(f[k].w);
+    uint32_t inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t up = __shfl_up(inc, o);
+      if (lane >= o) inc += up;
+    }
+    if (lane == 63) wtot[wave] = inc;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (int w = 0; w < 4; w++) {
+      before += w < wave ? wtot[w] : 0u;
+      total += wtot[w];
+    }
+    if (threadIdx.x == 0 && total) sbase = atomicAdd(nretry + 1, total);
+    __syncthreads();
+    if (c) {
+      int64_t o = (int64_t)sbase + before + inc - c;
+#pragma unroll
+      for (int k = 0; k < kMarkPer / 16; k++) {
+        const uint32_t w4[4] = {f[k].x, f[k].y, f[k].z, f[k].w};
+        for (int j = 0; j < 16; j++)
+          if ((w4[j >> 2] >> (8 * (j & 3))) & 0xFFu) retry[nq - 1 - o++] = (uint32_t)(rb + 16 * k + j);
+      }
+    }
+    __syncthreads();   // wtot / sbase reused by the next chunk
+  }
+}
+
+// The follower retries (kSeedGuess): every follower whose guessed cut-off held
+// fewer than K photons, re-walked with its guaranteed cut-off exactly as the
+// follower launch would have (same cut-off, walk and epilogue). A fixed grid
+// strides over the list, whose length only the device knows; every wave leaves
+// once the block's next chunk starts past it.
+template <int TAG, bool WIDE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_gather_fretry(
+    const float4* __restrict__ nodes, const float4* __restrict__ payload, int n, const float4* __restrict__ qb,
+    int64_t nq, float4* __restrict__ out, const uint32_t* __restrict__ perm, const float4* __restrict__ lead,
+    const uint32_t* __restrict__ fretry, const uint32_t* __restrict__ nfretry, BoxView bx) {
+  __shared__ double lq[(kGatherQL + 1) * 256];
+  const float R2 = kKMaxDistance * kKMaxDistance;
+  const uint32_t cnt = *nfretry;
+  for (uint32_t base = blockIdx.x * 256u; base < cnt; base += gridDim.x * 256u) {
+    const uint32_t e = base + threadIdx.x;
+    const bool valid = e < cnt;
+    const int64_t r = valid ? (int64_t)fretry[-(int64_t)e] : 0;
+    const int64_t i = !valid ? 0 : (perm ? (int64_t)perm[r] : r);
+    const float4 qq = valid ? qb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const v3 q = {qq.x, qq.y, qq.z};
+    // the guaranteed cut-off, or the own-subtree one where tighter (both hold
+    // the K nearest: the walk's result is the same)
+    float cut = lean_cut(R2);
+    if (valid) cut = fminf(follower_cut<kSeedGroup>(lead, nq, r, q, R2), subtree_cut<WIDE>(nodes, (uint32_t)n, q, cut));
+    double list[kKNearest];
+    if (kGatherBox == 2 || kGatherBox == 3)
+      knn_walk_lean<kKNearest, kGatherQL, WIDE, 0, kBoxAfter>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256,
+                                                              bx, nullptr);
+    else
+      knn_walk_lean<kKNearest, kGatherQL, WIDE, 0>(nodes, n, q, cut, valid, list, lq + threadIdx.x, 256, {}, nullptr);
+    if (valid) {
+      const bool full = gkey_word(list[kKNearest - 1]) != kNoWord;
+      const v3 f = radiance_g(list, payload, qq.w, full ? gkey_d2(list[kKNearest - 1]) : R2);
+      out[i] = make_float4(f.x, f.y, f.z, 0.f);
     }
   }
 }
@@ -896,9 +1057,19 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
 #else
   const int64_t nl = Seeds<kSeedGroup>::count(nq);   // leaders: walk ranks 0, S, 2S, ... (G = 1)
   DevBuf<float4> lead(nl);
-  DevBuf<uint32_t> retry(kLeaderBudget > 0 ? nl : 0), nretry(kLeaderBudget > 0 ? 1 : 0);
-  if (!lead.p || (kLeaderBudget > 0 && (!retry.p || !nretry.p))) return hipErrorOutOfMemory;
-  if (kLeaderBudget > 0) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, sizeof(uint32_t), s));
+  const int64_t nf = nq - nl;
+  // retry lists: the leaders cut off by their budget (upwards from entry 0,
+  // count nretry[0] <= nl), the followers whose guessed cut-off missed
+  // (kSeedGuess; downwards from entry nq - 1, count nretry[1] <= nq - nl)
+  const bool lists = kLeaderBudget > 0 || kSeedGuess;
+  DevBuf<uint32_t> retry(lists ? (kSeedGuess ? nq : nl) : 0), nretry(lists ? 2 : 0);
+  if (!lead.p || (lists && (!retry.p || !nretry.p))) return hipErrorOutOfMemory;
+  if (lists) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, 2 * sizeof(uint32_t), s));
+  DevBuf<uint8_t> missed(kSeedGuess && nf > 0 ? (size_t)nq + 4 : 0);   // follower miss flags by walk rank
+  if (kSeedGuess && nf > 0) {
+    if (!missed.p) return hipErrorOutOfMemory;
+    PM_HIP_TRY(hipMemsetAsync(missed.p, 0, (size_t)nq + 4, s));
+  }
   DevBuf<float4> box(kGatherBox ? 2 * (size_t)std::max<int64_t>(boxed_nodes(n, PM_GATHER_BOX_SKIP), 1) : 0);
   BoxView bx;
   hipEvent_t box_done = nullptr;
@@ -957,24 +1128,23 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
     box_done = nullptr;
     return e;
   };
-  const int64_t nf = nq - nl;
   // node byte offsets fit 32 bits below 2^28 nodes (saddr loads); larger maps use 64-bit addresses
   const bool wide = PM_FORCE_WIDE || n >= (1 << 28);
-  uint32_t* const rt = kLeaderBudget > 0 ? retry.p : nullptr;
-  uint32_t* const nrt = kLeaderBudget > 0 ? nretry.p : nullptr;
+  uint32_t* const rt = lists ? retry.p : nullptr;
+  uint32_t* const nrt = lists ? nretry.p : nullptr;
   // one launch of k_gather_level<tag, LEADERS, wide> over lanes [0, t1)
   auto level = [&](auto leaders, int grid, int rb, int64_t t1) -> hipError_t {
     constexpr bool L = decltype(leaders)::value;
     if (grid <= 0) return hipSuccess;
     const float4 *nd = m->nodes.p, *pl = m->payload.p;
     if (tag == 1 && wide)
-      k_gather_level<1, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
+      k_gather_level<1, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, missed.p);
     else if (tag == 1)
-      k_gather_level<1, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
+      k_gather_level<1, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, missed.p);
     else if (wide)
-      k_gather_level<0, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
+      k_gather_level<0, L, true><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, missed.p);
     else
-      k_gather_level<0, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1);
+      k_gather_level<0, L, false><<<grid, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, rt, nrt, rb, bx, t1, missed.p);
     return hipGetLastError();
   };
   // leaders (walk ranks 0, S, 2S, ...), then the followers with the retry
@@ -983,6 +1153,18 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   PM_HIP_TRY(boxes_ready());
   const int rb = kLeaderBudget > 0 ? grid_for(nl, 256) : 0;
   if (nf > 0 || kLeaderBudget > 0) PM_HIP_TRY(level(std::false_type{}, grid_for(nf, 256) + rb, rb, nf));
+  if (kSeedGuess && nf > 0) {   // the guessed cut-offs that missed, re-walked with the guaranteed ones
+    k_gather_fmark<<<(int)std::min<int64_t>(grid_for(nq, 256 * kMarkPer), 2048), 256, 0, s>>>(missed.p, nq, retry.p,
+                                                                                           nretry.p);
+    PM_HIP_TRY(hipGetLastError());
+    const int g = (int)std::min<int64_t>(grid_for(nf, 256), 1024);
+    const float4 *nd = m->nodes.p, *pl = m->payload.p;
+    const uint32_t *fr = retry.p + nq - 1, *nfr = nretry.p + 1;   // the list runs downwards from fr
+    if (tag == 1 && wide) k_gather_fretry<1, true><<<g, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, fr, nfr, bx);
+    else if (tag == 1) k_gather_fretry<1, false><<<g, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, fr, nfr, bx);
+    else if (wide) k_gather_fretry<0, true><<<g, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, fr, nfr, bx);
+    else k_gather_fretry<0, false><<<g, 256, 0, s>>>(nd, pl, n, qb, nq, out, perm, lead.p, fr, nfr, bx);
+  }
   return hipGetLastError();
 #endif
 }
@@ -1493,3 +1675,4 @@ hipError_t launch_gather_api(const pm_photon_map* m, const pm_float3* pts, const
 }
 
 }  // namespace pmd
+

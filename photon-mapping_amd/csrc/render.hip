@@ -285,6 +285,9 @@ __global__ __launch_bounds__(kRBlock) PM_WAVES_ATTR(PM_PATHS_WAVES) void k_paths
 // Final-gather rays: closest hit from the vertex; a hit with a diffuse
 // material yields a global-map query (hitpoint, brdf) and its albedo
 // (closestHit + deviceCode.cu:120-129).
+#ifndef PM_RAYS_LDS_PAD
+#define PM_RAYS_LDS_PAD 0   // extra LDS bytes per ray-pool workgroup (caps workgroups per CU)
+#endif
 #ifndef PM_RAYS_WAVES
 #define PM_RAYS_WAVES 8   // occupancy target of k_diffuse_rays / k_shadow_rays (0: compiler's choice; 8 with 64-B nodes)
 #endif
@@ -769,7 +772,7 @@ hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light*
     PhaseTimer tm(PH_PATHS, s);
     if (NG > 0) {
       if (PM_RAY_POOL)
-        k_diffuse_rays_pool<<<grid_for(NG, pool_chunk(NG, kRBlock)), kRBlock, 0, s>>>(
+        k_diffuse_rays_pool<<<grid_for(NG, pool_chunk(NG, kRBlock)), kRBlock, PM_RAYS_LDS_PAD, s>>>(
             S, J->cq.p, J->gdir.p, NG, J->gvalid.p, J->gq.p, J->galb.p, sc->overflow.p, pool_chunk(NG, kRBlock));
       else
         k_diffuse_rays<<<grid_for(NG, kRBlock), kRBlock, 0, s>>>(S, J->cq.p, J->gdir.p, NG, J->gvalid.p, J->gq.p,
@@ -778,7 +781,7 @@ hipError_t render_begin(pm_scene* sc, const pm_render_params* P, const pm_light*
     }
     if (NS > 0) {
       if (PM_RAY_POOL)
-        k_shadow_rays_pool<<<grid_for(NS, pool_chunk(NS, kRBlock)), kRBlock, 0, s>>>(
+        k_shadow_rays_pool<<<grid_for(NS, pool_chunk(NS, kRBlock)), kRBlock, PM_RAYS_LDS_PAD, s>>>(
             S, J->cq.p, J->sray.p, nl, NS, J->svis.p, sc->overflow.p, pool_chunk(NS, kRBlock));
       else
         k_shadow_rays<<<grid_for(NS, kRBlock), kRBlock, 0, s>>>(S, J->cq.p, J->sray.p, nl, NS, J->svis.p,

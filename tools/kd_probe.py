@@ -2,6 +2,9 @@
 written to OUT.npz, and the build time of a config-3-sized map.
     python3 tools/kd_probe.py OUT.npz [--time]
     python3 tools/kd_probe.py --compare A.npz B.npz
+    python3 tools/kd_probe.py --stamps   (a -DPM_KD_DIAG_TIME library: config 3's
+        photon sets traced, the global map built, k_kd_local_sel's per-phase
+        clock64 stamps averaged over its workgroups)
 Shapes: sizes around the local-finish threshold (1023 / 1024 / 2047 / 2048),
 uniform clouds, planes of ties, exact duplicates, one repeated point, a few
 distinct values, +inf coordinates and negative zeros."""
@@ -112,7 +115,37 @@ def compare(a, b):
     return bad
 
 
+def stamps():
+    import ctypes
+    import torch
+    import pm_amd
+    from pm_amd import scenes
+    meshes, lights = scenes.sponza_class()
+    scene = pm_amd.Scene(meshes)
+    g, c = pm_amd.run_photon_sets(scene, lights, 10_000_000, 1_000_000, 30)
+    names = ["load + extents", "block level 0", "block level 1", "block level 2", "block level 3",
+             "wave sorts", "wave levels + write-out"]
+    fn = pm_amd._lib.pm_diag_kd_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+    for rep in range(3):
+        m = pm_amd.PhotonMap(g, 1.0, c, 0.5)
+        torch.cuda.synchronize()
+        buf = np.zeros(65536 * 8, np.uint64)
+        assert fn(buf.ctypes.data, buf.size) == 0
+        st = buf.reshape(-1, 8).astype(np.int64)
+        ok = (st[:, 0] > 0) & (st[:, 7] >= st[:, 0]) & np.all(st[:, 1:] > 0, axis=1)
+        d = np.diff(st[ok], axis=1)
+        tot = st[ok, 7] - st[ok, 0]
+        print(f"rep {rep}: {ok.sum()} workgroups, kdbuild {pm_amd.phase_us('kdbuild') / 1e3:.2f} ms, "
+              f"mean {tot.mean():.0f} clocks per workgroup", flush=True)
+        for k, nm in enumerate(names):
+            print(f"   {nm:26s} {d[:, k].mean():9.0f} clocks  {100 * d[:, k].mean() / tot.mean():5.1f} %", flush=True)
+        del m
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "--stamps":
+        sys.exit(stamps())
     if sys.argv[1] == "--compare":
         sys.exit(1 if compare(sys.argv[2], sys.argv[3]) else 0)
     run(sys.argv[1], "--time" in sys.argv)
