@@ -630,15 +630,18 @@ constexpr int kBoxAfter = PM_BOX_AFTER;
 // follower f and any leader L: seed_bound. It is loose wherever the density
 // varies slowly, which is almost everywhere: a follower walks with the tighter
 // GUESS min(r_L + d, r_L (1 + beta) + alpha d) instead. A follower whose list
-// does not fill under a guess (fewer than K photons inside it) is not written:
-// its walk rank goes to a retry list, and k_gather_fretry re-walks it with the
-// guaranteed cut-off after the follower launch. A list that does fill holds
+// does not fill under a guess (fewer than K photons inside it) flags its walk
+// rank; k_gather_fmark lists the flags and k_gather_fretry re-walks them with
+// the guaranteed (or own-subtree, if tighter) cut-off after the follower
+// launch, overwriting their slots. A list that does fill holds
 // the K nearest (every point inside the cut-off was visited), the same keys
 // the guaranteed walk finds, so every result is bitwise the production one.
-// Config 3 (guess only, misses not re-walked; profiles/r06/r06k_*): alpha /
-// beta 0.5 / 0.1: 0.009 % misses, 0.25 / 0.1: 0.33 % (gather -2.2 ms), 0 / 0.3:
-// 3 % (-3.7 ms), 0 / 0.2: 10 % (-5.2 ms); a retried walk costs about what a
-// leader's does (~3 follower walks: its neighbours in the retry list are far).
+// Config 3 (profiles/r06/r06k_seed_guess_*): the misses of alpha / beta
+// 0.5 / 0.1: 0.009 %, 0.25 / 0.1: 0.33 %, 0 / 0.3: 3 %, 0 / 0.2: 10 %; with
+// the retries, the global gather 40.3 ms (guaranteed only) -> 37.1 (0.25 /
+// 0.1), 36.8 (0.25 / 0.075), 37.1 (0.2 / 0.075, 0.25 / 0.05), 37.5 (0.3 /
+// 0.025), 38.6-39.3 (0.15 / 0.05), 47.0 (0 / 0.3): a retried walk costs ~10
+// follower walks (it runs nearly alone: the retries are scattered).
 #ifndef PM_SEED_GUESS
 #define PM_SEED_GUESS 1
 #endif
@@ -646,9 +649,17 @@ constexpr int kBoxAfter = PM_BOX_AFTER;
 #define PM_SEED_GUESS_ALPHA 0.25
 #endif
 #ifndef PM_SEED_GUESS_BETA
-#define PM_SEED_GUESS_BETA 0.1
+#define PM_SEED_GUESS_BETA 0.075
+#endif
+// Follower launches of fewer walks guess nothing: the retry launch costs about
+// one walk's latency (~0.7-1 ms) whatever the misses, more than the guess saves
+// on a short launch (config 2, 3.7 M queries: global gather 4.2 -> 5.3 ms with
+// guesses; config 3, 36 M: 40.3 -> 36.8; config 5, 45 M: 49.2 -> 46.8-47.9)
+#ifndef PM_SEED_GUESS_MIN
+#define PM_SEED_GUESS_MIN (1 << 23)
 #endif
 constexpr bool kSeedGuess = PM_SEED_GUESS;
+constexpr int64_t kSeedGuessMin = PM_SEED_GUESS_MIN;
 __device__ __forceinline__ double seed_sq(double c) { return c * c * (1.0 + 1e-5) + 1e-30; }
 // (guaranteed, guessed) squared bounds of follower q from one leader record
 __device__ __forceinline__ void seed_bounds(float4 lead, v3 q, double& guar, double& guess) {
@@ -1061,12 +1072,13 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   // retry lists: the leaders cut off by their budget (upwards from entry 0,
   // count nretry[0] <= nl), the followers whose guessed cut-off missed
   // (kSeedGuess; downwards from entry nq - 1, count nretry[1] <= nq - nl)
-  const bool lists = kLeaderBudget > 0 || kSeedGuess;
-  DevBuf<uint32_t> retry(lists ? (kSeedGuess ? nq : nl) : 0), nretry(lists ? 2 : 0);
+  const bool guess = kSeedGuess && nf > 0 && nf >= kSeedGuessMin;
+  const bool lists = kLeaderBudget > 0 || guess;
+  DevBuf<uint32_t> retry(lists ? (guess ? nq : nl) : 0), nretry(lists ? 2 : 0);
   if (!lead.p || (lists && (!retry.p || !nretry.p))) return hipErrorOutOfMemory;
   if (lists) PM_HIP_TRY(hipMemsetAsync(nretry.p, 0, 2 * sizeof(uint32_t), s));
-  DevBuf<uint8_t> missed(kSeedGuess && nf > 0 ? (size_t)nq + 4 : 0);   // follower miss flags by walk rank
-  if (kSeedGuess && nf > 0) {
+  DevBuf<uint8_t> missed(guess ? (size_t)nq + 4 : 0);   // follower miss flags by walk rank
+  if (guess) {
     if (!missed.p) return hipErrorOutOfMemory;
     PM_HIP_TRY(hipMemsetAsync(missed.p, 0, (size_t)nq + 4, s));
   }
@@ -1153,7 +1165,7 @@ hipError_t launch_gather(const pm_photon_map* m, const float4* qb, int64_t nq, f
   PM_HIP_TRY(boxes_ready());
   const int rb = kLeaderBudget > 0 ? grid_for(nl, 256) : 0;
   if (nf > 0 || kLeaderBudget > 0) PM_HIP_TRY(level(std::false_type{}, grid_for(nf, 256) + rb, rb, nf));
-  if (kSeedGuess && nf > 0) {   // the guessed cut-offs that missed, re-walked with the guaranteed ones
+  if (guess) {   // the guessed cut-offs that missed, re-walked with the guaranteed ones
     k_gather_fmark<<<(int)std::min<int64_t>(grid_for(nq, 256 * kMarkPer), 2048), 256, 0, s>>>(missed.p, nq, retry.p,
                                                                                            nretry.p);
     PM_HIP_TRY(hipGetLastError());
