@@ -61,8 +61,9 @@ def host_cores():
 def cpu_baseline(meshes, lights, args, n_global_full, nthreads, full_photons=None):
     """Scalar oracle (oracle/libpm_oracle.so, pthreads) on a bounded sample of the
     same workload, scaled linearly to one frame. full_photons = (diffuse,
-    caustic) pm_photon arrays of the whole frame (the GPU trace's, bitwise the
-    oracle's: tests/test_gpu_fullsize.py): the maps are then built from all of
+    caustic) pm_photon arrays of the whole frame (the GPU trace's; three 1 %
+    id-shards of the same full-size trace are checked bitwise against the
+    oracle's in tests/test_gpu_fullsize.py, not the whole array): the maps are then built from all of
     them (timed, not scaled) and the sampled rows are rendered over maps of the
     frame's own photon density; without them, maps of the traced sample."""
     import numpy as np
@@ -101,8 +102,8 @@ def cpu_baseline(meshes, lights, args, n_global_full, nthreads, full_photons=Non
         "value": P / total / 1e6, "unit": "Mphotons/s", "cores": nthreads, "kind": "port",
         "nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
         "sample": (f"oracle (pthreads x{nthreads}) traced {sg + scn} of {P} photons (scaled x{1 / frac:.1f}), "
-                   + (f"kd-built the frame's full maps ({n_s} photons, the GPU trace's photons, bitwise the "
-                      f"oracle's), rendered {rows} of {args.height} rows at {args.width} px (scaled "
+                   + (f"kd-built the frame's full maps ({n_s} photons: the GPU trace's, whose 1 % id-shards "
+                      f"0/37/99 tests/test_gpu_fullsize.py checks bitwise against the oracle's), rendered {rows} of {args.height} rows at {args.width} px (scaled "
                       f"x{args.height / rows:.1f}) over those full-density maps"
                       if full_photons is not None and n_s == n_global_full else
                       f"kd-built {n_s} photons (scaled N log N to {n_global_full}), rendered {rows} of "
